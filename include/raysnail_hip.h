@@ -1,0 +1,210 @@
+/*
+ * raysnail_hip.h — C-ABI of libraysnail_hip.so, the MI355X (gfx950) render path.
+ *
+ * This is the drop-in boundary for raysnail's per-pixel render path
+ *   Painter::draw sample loop -> Camera::ray -> Hittable::hit (BVH) -> Material::scatter/emitted
+ * (reference: src/camera.rs:261-287 TakePhotoSettings::shot_to_target, src/painter.rs:307-336
+ * Painter::draw). The GPU cannot call a Rust closure, so the boundary sits at shot_to_target
+ * level: the caller flattens World + Camera + settings into plain-old-data through the calls
+ * below, then asks for a frame. Every entry point is extern "C", takes plain pointers and sizes,
+ * returns an int status (0 = ok, <0 = error) and never throws or aborts across the ABI;
+ * rs_last_error() returns a thread-local message for the last failure on the calling thread.
+ *
+ * Reference interfaces replaced (file:line in Varkalandar/raysnail @ 2024-10-08):
+ *   rs_scene_create/destroy  World::new                      src/hittable/collection/world.rs:40-53
+ *   rs_material              Lambertian/Metal/DiffuseMetal/Dielectric/DiffuseLight/MixedMaterial
+ *                            constructors                      src/material/{lambertian.rs:29-35,
+ *                            metal.rs:43-49 (DiffuseMetal), metal.rs:95-100 (Metal), dielectric.rs:38-53,
+ *                            light.rs:17-28, mixed_material.rs:32-38}; textures Color / Checker
+ *                            src/prelude/color.rs:61-65, src/texture/checker.rs:16-18;
+ *                            CommonMaterialSettings src/material/mod.rs:41-54
+ *   rs_sphere                Sphere::new / with_speed         src/hittable/geometry/sphere.rs:35-48
+ *   rs_aarect                AARect::new_xy/new_xz/new_yz     src/hittable/geometry/rect.rs:58-79
+ *   rs_box                   Box::new                         src/hittable/geometry/box.rs:40-45
+ *   rs_quadric               Quadric::new                     src/hittable/geometry/quadric.rs:46-61
+ *   rs_triangles             Triangle::new + set_normals      src/hittable/geometry/triangle_mesh.rs:42-71
+ *   rs_intersection          Intersection::new                src/hittable/csg/intersection.rs:33-39
+ *   rs_difference            Difference::new                  src/hittable/csg/difference.rs:32-38
+ *   rs_transformed           TfFacade::new + TransformStack   src/hittable/transform/tf_facade.rs:30-37,
+ *                                                             transform.rs:16-127
+ *   rs_world_add             HittableList::add (world list)   src/hittable/collection/list.rs:29-33
+ *   rs_lights_add            HittableList::add (lights list)  src/hittable/collection/list.rs:29-33
+ *   rs_set_background        World background closure         examples/rtow_13_1.rs:38-41,
+ *                                                             src/bin/raysnail.rs:364-367
+ *   rs_render                TakePhotoSettings::shot_to_target src/camera.rs:261-287 (CameraBuilder
+ *                            src/camera.rs:300-413; Painter src/painter.rs:69-336)
+ *   rs_render_device         same, with the frame left in device memory (no PCIe in the timed region)
+ *
+ * Output layout is the reference's Vec<[f32;4]>: W*H RGBA float32, row-major, row 0 = top,
+ * sqrt-gamma applied when gamma != 0, unclamped, alpha 1.0 for rendered pixels, [0,0,0,0] for
+ * pixels whose mask byte is 0 (PixelController::calculate_pixel == false, src/painter.rs:204-210).
+ * Rows outside [row_begin, row_end) or not on the row_step lattice are left untouched.
+ *
+ * Determinism contract (the reference has none: every FastRng is seeded from thread_rng,
+ * src/prelude/random.rs:116-121). Sample s of pixel p (linear index y*W+x) draws from its own
+ * XorShift128 stream, seeded with rand_core-0.6 seed_from_u64(rs_stream_key(seed, pass, p, s)).
+ * Within a sample, draws follow the reference order exactly: render_pixel jitter x then y
+ * (painter.rs:167-170), Camera::ray disk rejection + shutter time (camera.rs:77-85), then per
+ * bounce of ray_color (camera.rs:156-255). thread_rng draws on the path are taken from the same
+ * stream at the same point: Dielectric's Random::normal (dielectric.rs:72) as one gen(),
+ * MixedMaterial's next_u32 (mixed_material.rs:44) as one next_u32().
+ */
+#ifndef RAYSNAIL_HIP_H
+#define RAYSNAIL_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define RS_OK             0
+#define RS_E_INVALID     -1  /* bad argument / handle */
+#define RS_E_NO_LIGHTS   -2  /* a pdf material exists but the lights list is empty (ref: % 0 panic, list.rs:51) */
+#define RS_E_HIP         -3  /* HIP runtime error */
+#define RS_E_STATE       -4  /* call not allowed in this state (e.g. render before commit) */
+#define RS_E_UNSUPPORTED -5  /* construct outside what the GPU path implements */
+#define RS_E_NOMEM       -6
+
+/* ---- textures (src/prelude/color.rs:61-65, src/texture/checker.rs:21-30) ---- */
+#define RS_TEX_SOLID   0
+#define RS_TEX_CHECKER 1
+typedef struct rs_texture_desc {
+    int32_t kind;     /* RS_TEX_SOLID: color = even; RS_TEX_CHECKER: sin(sx)sin(sy)sin(sz) < 0 ? odd : even */
+    int32_t _pad;
+    float   even[4];  /* rgba */
+    float   odd[4];   /* rgba */
+    double  scale;    /* checker frequency */
+} rs_texture_desc;
+
+/* ---- materials (src/material/ *.rs) ---- */
+#define RS_MAT_LAMBERTIAN    0
+#define RS_MAT_METAL         1
+#define RS_MAT_DIFFUSE_METAL 2
+#define RS_MAT_DIELECTRIC    3
+#define RS_MAT_DIFFUSE_LIGHT 4
+#define RS_MAT_MIXED         5
+#define RS_NO_MATERIAL      (-1)  /* Option<Arc<dyn Material>> = None */
+
+typedef struct rs_material_desc {
+    int32_t kind;
+    int32_t glass;            /* Dielectric: 1 = .reflect_curve(Glass{}) (Schlick), 0 = none */
+    rs_texture_desc texture;  /* albedo / light texture; Dielectric tint = texture.even */
+    double  refractive;       /* Dielectric refractive index */
+    double  exponent;         /* DiffuseMetal phong-lobe exponent */
+    double  multiplier;       /* DiffuseLight multiplier */
+    int32_t mix_a, mix_b;     /* MixedMaterial: material ids (already created) */
+    double  mix_p;            /* MixedMaterial probability of mix_a */
+    double  phong_factor;     /* CommonMaterialSettings.phong_factor (0 = off) */
+    int32_t phong_exponent;   /* CommonMaterialSettings.phong_exponent */
+    int32_t _pad;
+} rs_material_desc;
+
+/* ---- geometry ---- */
+#define RS_PLANE_XY 0   /* AARect::new_xy: axes (0,1), fixed 2 */
+#define RS_PLANE_XZ 1   /* AARect::new_xz: axes (0,2), fixed 1 */
+#define RS_PLANE_YZ 2   /* AARect::new_yz: axes (1,2), fixed 0 */
+
+#define RS_TF_TRANSLATE 0 /* v = offset */
+#define RS_TF_ROTATE_X  1 /* v[0] = angle in radians (Transform::rotate_by_x_axis) */
+#define RS_TF_ROTATE_Y  2
+#define RS_TF_ROTATE_Z  3
+#define RS_TF_SCALE     4 /* v = factors */
+typedef struct rs_transform {
+    int32_t kind;
+    int32_t _pad;
+    double  v[3];
+} rs_transform;
+
+/* ---- camera (CameraBuilder, src/camera.rs:300-413) ---- */
+typedef struct rs_camera_desc {
+    double   look_from[3];
+    double   look_at[3];
+    double   vup[3];
+    double   fov;        /* vertical field of view, degrees */
+    double   aperture;
+    double   focus;      /* focus distance */
+    double   shutter;    /* shutter speed (ray time = shutter * gen()) */
+    uint32_t width, height;
+} rs_camera_desc;
+
+/* ---- render settings (TakePhotoSettings src/camera.rs:104-154 + Painter src/painter.rs:69-130) ---- */
+#define RS_MODE_AUTO      0
+#define RS_MODE_MEGAKERNEL 1  /* one thread per path, all bounces in one launch */
+#define RS_MODE_WAVEFRONT  2  /* extend / shade kernels over SoA path queues */
+typedef struct rs_render_settings {
+    uint32_t samples;    /* requested spp; N = floor(sqrt(samples))^2 is rendered (painter.rs:110-118) */
+    uint32_t depth;      /* ray_color recursion depth (default 8, camera.rs:118) */
+    int32_t  gamma;      /* 1 = sqrt gamma (into_color, vec3.rs:227-240) */
+    int32_t  mode;       /* RS_MODE_* */
+    uint64_t seed;       /* frame seed of the determinism contract */
+    uint32_t pass;       /* progressive pass index (mixes into the stream key) */
+    uint32_t row_begin;  /* rows [row_begin, row_end) with stride row_step are rendered */
+    uint32_t row_end;    /* 0 = height */
+    uint32_t row_step;   /* 0 or 1 = every row */
+} rs_render_settings;
+
+typedef struct rs_render_stats {
+    uint64_t samples;    /* camera samples traced */
+    uint64_t segments;   /* world.hit calls (path segments) */
+    double   ms;         /* wall time inside the call (device work + sync) */
+} rs_render_stats;
+
+typedef struct rs_scene rs_scene;
+
+/* ---- library ---- */
+int         rs_abi_version(void);
+const char* rs_last_error(void);
+int         rs_device_count(int* count);
+uint64_t    rs_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample);
+
+/* ---- scene construction ---- */
+int rs_scene_create(rs_scene** out);
+int rs_scene_destroy(rs_scene* s);
+int rs_material(rs_scene* s, const rs_material_desc* desc, int32_t* id_out);
+int rs_sphere(rs_scene* s, const double center[3], double radius, const double speed[3] /* NULL = 0 */,
+              int32_t material, uint32_t* handle_out);
+int rs_aarect(rs_scene* s, int32_t plane, double k, double a0, double a1, double b0, double b1,
+              int32_t material, uint32_t* handle_out);
+int rs_box(rs_scene* s, const double p0[3], const double p1[3], int32_t material, uint32_t* handle_out);
+int rs_quadric(rs_scene* s, const double q[10] /* qa qb qc qd qe qf qg qh qi qj */, int32_t material,
+               uint32_t* handle_out);
+/* n triangles; pos = n*9 doubles (p0 p1 p2); nrm = n*9 doubles (n0 n1 n2) or NULL (zero normals,
+ * Triangle::new default); handles are first_out .. first_out+n-1 */
+int rs_triangles(rs_scene* s, const double* pos, const double* nrm, uint32_t n, int32_t material,
+                 uint32_t* first_out);
+int rs_intersection(rs_scene* s, uint32_t a, uint32_t b, int32_t material, uint32_t* handle_out);
+int rs_difference(rs_scene* s, uint32_t plus, uint32_t minus, int32_t material, uint32_t* handle_out);
+int rs_transformed(rs_scene* s, uint32_t object, const rs_transform* stack, uint32_t n, uint32_t* handle_out);
+int rs_world_add(rs_scene* s, uint32_t handle);
+int rs_lights_add(rs_scene* s, uint32_t handle);
+int rs_set_background(rs_scene* s, const float lo[3], const float hi[3]);
+/* World::new time_limit (world.rs:40-53): bounding boxes of moving spheres span [t0, t1];
+ * the reference passes 0..camera.shutter_speed. Default [0, 0]. */
+int rs_set_time_range(rs_scene* s, double t0, double t1);
+/* freeze the scene: build the BVH and upload it to the current HIP device */
+int rs_scene_commit(rs_scene* s);
+
+/* ---- render ---- */
+/* host output: out_rgba = W*H*4 floats; mask = W*H bytes or NULL (all pixels) */
+int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st,
+              const uint8_t* mask, float* out_rgba, rs_render_stats* stats);
+/* device output: d_out_rgba device pointer (W*H*4 floats), d_mask device pointer or NULL,
+ * stream = hipStream_t or NULL (default stream). Returns after the work is enqueued AND
+ * complete (the call synchronises its stream) so that stats are final. */
+int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st,
+                     const uint8_t* d_mask, float* d_out_rgba, void* stream, rs_render_stats* stats);
+
+/* ---- diagnostics (parity probes used by tests/) ---- */
+/* World::hit (world.rs:63-65) for n rays on the device. rays: n*7 doubles (origin, direction,
+ * time); out: n*13 doubles = [hit, t1, t2, p.xyz, n.xyz, u, v, outside, material id] (u, v are
+ * not computed on the GPU: 0). tmax must be +inf or the hit is dropped when t1 >= tmax. */
+int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin, double tmax, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAYSNAIL_HIP_H */

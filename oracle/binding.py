@@ -1,0 +1,107 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from raysnail_amd import _abi as A
+from raysnail_amd.api import World, realize, _check
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+_LIB = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def load() -> C.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in A.SCENE_SIGNATURES.items():
+        f = getattr(lib, "orc_" + name)
+        f.restype, f.argtypes = res, args
+    lib.orc_last_error.restype = C.c_char_p
+    lib.orc_scene_create.restype = C.c_void_p
+    lib.orc_scene_destroy.argtypes = [C.c_void_p]
+    lib.orc_commit.argtypes = [C.c_void_p]
+    lib.orc_commit.restype = C.c_int
+    lib.orc_render.argtypes = [C.c_void_p, C.POINTER(A.rs_camera_desc), C.POINTER(A.rs_render_settings), C.c_void_p,
+                               C.c_void_p, C.c_int, C.POINTER(A.rs_render_stats)]
+    lib.orc_render.restype = C.c_int
+    lib.orc_sample_radiance.argtypes = [C.c_void_p, C.POINTER(A.rs_camera_desc), C.POINTER(A.rs_render_settings),
+                                        C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_uint64)]
+    lib.orc_sample_radiance.restype = C.c_int
+    lib.orc_stream_key.restype = C.c_uint64
+    lib.orc_stream_key.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]
+    lib.orc_rng_u32.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32)]
+    lib.orc_rng_u32_from_words.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]
+    lib.orc_rng_gen.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]
+    lib.orc_world_hit.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double, C.c_double,
+                                  C.c_double, C.POINTER(C.c_double)]
+    lib.orc_world_hit.restype = C.c_int
+    lib.orc_tf_apply.argtypes = [C.POINTER(A.rs_transform), C.c_uint32, C.POINTER(C.c_double), C.c_double, C.c_int,
+                                 C.POINTER(C.c_double)]
+    lib.orc_camera_ray.argtypes = [C.POINTER(A.rs_camera_desc), C.c_double, C.c_double, C.c_uint64,
+                                   C.POINTER(C.c_double)]
+    lib.orc_scatter.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_uint64,
+                                C.POINTER(C.c_double)]
+    lib.orc_scatter.restype = C.c_int
+    _LIB = lib
+    return lib
+
+
+class OracleScene:
+    """The same World replayed into the CPU restatement."""
+
+    def __init__(self, world: World):
+        self.lib = load()
+        self.h = C.c_void_p(self.lib.orc_scene_create())
+        realize(world, self.lib, self.h, "orc_")
+        _check(self.lib, self.lib.orc_commit(self.h), "orc_")
+
+    def __del__(self):
+        try:
+            self.lib.orc_scene_destroy(self.h)
+        except Exception:
+            pass
+
+    def render(self, cam: A.rs_camera_desc, st: A.rs_render_settings, threads: int = 0, mask=None, out=None):
+        H, W = cam.height, cam.width
+        if out is None:
+            out = np.zeros((H, W, 4), dtype=np.float32)
+        mptr = None
+        if mask is not None:
+            mask = np.ascontiguousarray(mask, dtype=np.uint8).reshape(H * W)
+            mptr = mask.ctypes.data_as(C.c_void_p)
+        stats = A.rs_render_stats()
+        _check(self.lib, self.lib.orc_render(self.h, C.byref(cam), C.byref(st), mptr,
+                                             out.ctypes.data_as(C.c_void_p), threads, C.byref(stats)), "orc_")
+        return out, stats
+
+    def sample_radiance(self, cam, st, x, y, s):
+        out = (C.c_double * 3)()
+        seg = C.c_uint64()
+        _check(self.lib, self.lib.orc_sample_radiance(self.h, C.byref(cam), C.byref(st), x, y, s, out, C.byref(seg)),
+               "orc_")
+        return np.array(list(out)), seg.value
+
+    def world_hit(self, o, d, time=0.0, tmin=1e-4, tmax=float("inf")):
+        out = (C.c_double * 13)()
+        _check(self.lib, self.lib.orc_world_hit(self.h, (C.c_double * 3)(*o), (C.c_double * 3)(*d), time, tmin, tmax,
+                                                out), "orc_")
+        return list(out)

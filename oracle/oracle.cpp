@@ -1,0 +1,1307 @@
+// oracle/oracle.cpp — CPU restatement of raysnail's per-pixel render path.
+//
+// TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+// leg may load this library, and only as the checker (or the timed CPU baseline). The product
+// (raysnail_amd/, libraysnail_hip.so) never links or calls it.
+//
+// What it restates (Varkalandar/raysnail @ 2024-10-08; paths relative to the reference root):
+//   Painter::samples / calculate_uv / render_pixel / render_rows / draw   src/painter.rs:110-139,154-187,239-336
+//   Vec3 arithmetic (dot/length_squared via mul_add, unit = v*(1/len))     src/prelude/vec3.rs:140-240,486-500
+//   Color, gradient                                                       src/prelude/color.rs:11-58
+//   Ray::at (per-axis mul_add)                                            src/prelude/ray.rs:21-31
+//   AABB::hit slab test                                                   src/prelude/aabb.rs:20-38
+//   ONB::build_from / local                                               src/prelude/onb.rs:11-40
+//   CosinePdf, ReflectionPdf, random_cosine_direction(_exponent)          src/prelude/pdf.rs:20-141, vec3.rs:100-126
+//   FastRng (XorShiftRng of rand_xorshift 0.3.0, seed_from_u64 of rand_core 0.6) src/prelude/random.rs:109-145
+//   Camera::new / Camera::ray, phong_highlight, ray_color                src/camera.rs:37-100,156-255
+//   HitRecord::new / with_normal / set_material_if_none                   src/hittable/hit.rs:32-78
+//   World / BVH / HittableList::random                                    src/hittable/collection/{world.rs,bvh.rs,list.rs}
+//   Sphere, AARect, Box, Quadric, Triangle                                src/hittable/geometry/*.rs
+//   Intersection, Difference                                              src/hittable/csg/*.rs
+//   TfFacade, Transform, TransformStack                                   src/hittable/transform/*.rs
+//   Lambertian, Metal, DiffuseMetal, Dielectric(+Glass), DiffuseLight, MixedMaterial  src/material/*.rs
+//   Checker texture                                                       src/texture/checker.rs:21-30
+//
+// Deviations, all documented in DESIGN.md §Oracle:
+//   * RNG: the reference seeds every FastRng from the OS (thread_rng). Here sample s of pixel p
+//     gets its own FastRng seeded with seed_from_u64(rs_stream_key(seed, pass, p, s)); draw order
+//     inside a sample is the reference's. thread_rng draws on the path (Dielectric, Mixed) come
+//     from the same stream at the same point.
+//   * BVH: the reference picks a random split axis (bvh.rs:91) and puts two objects in one leaf
+//     without testing their own boxes. Here the axis is find_best_axis (bvh.rs:116-169, present
+//     but unused upstream) and every object sits in its own leaf, so the closest hit does not
+//     depend on tree shape.
+//   * Box::hit with >= 3 face hits aborts upstream (assert, box.rs:129); here the first two are used.
+//   * Unbounded rejection loops (disk, Sphere::random, ReflectionPdf::generate) are capped at
+//     RS_REJECTION_CAP tries, identically in the GPU path; the cap is never reached in practice.
+//
+// Third-party arithmetic restated without its source in the container (parity at these seams is
+// pinned only by published test vectors, see tests/test_oracle_kat.py):
+//   rand_xorshift 0.3.0 XorShiftRng (Cargo.lock:443-446), rand_core 0.6.2 seed_from_u64
+//   (Cargo.lock:425-427), vecmath 1.0.0 row_mat4_transform / mat4_inv (Cargo.lock:566-568),
+//   compiler-rt __powidf2 for runtime powi (phong), LLVM's constant powi(x,5) expansion (Glass).
+//
+// Build: oracle/Makefile (g++ -O2 -ffp-contract=off; FMA only where the reference calls mul_add).
+
+#include "../include/raysnail_hip.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#define RS_REJECTION_CAP 4096
+
+namespace orc {
+
+static const double PI = 3.14159265358979323846;
+
+// ---------------------------------------------------------------- Vec3 (vec3.rs) ----
+struct Vec3 {
+    double x = 0, y = 0, z = 0;
+    Vec3() = default;
+    Vec3(double a, double b, double c) : x(a), y(b), z(c) {}
+    double operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    double& operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+    // vec3.rs:152-155 length_squared = z.mul_add(z, x.mul_add(x, y*y))
+    double length_squared() const { return std::fma(z, z, std::fma(x, x, y * y)); }
+    double length() const { return std::sqrt(length_squared()); }
+    // vec3.rs:177-179
+    double dot(const Vec3& r) const { return std::fma(z, r.z, std::fma(x, r.x, y * r.y)); }
+    // vec3.rs:182-188
+    Vec3 cross(const Vec3& r) const {
+        return Vec3(y * r.z - z * r.y, z * r.x - x * r.z, x * r.y - y * r.x);
+    }
+    // vec3.rs:192-194 + Div<f64> = mul by reciprocal (vec3.rs:486-492)
+    Vec3 unit() const { return div(length()); }
+    Vec3 div(double s) const { double inv = 1.0 / s; return Vec3(x * inv, y * inv, z * inv); }
+    Vec3 operator-() const { return Vec3(-x, -y, -z); }
+};
+static inline Vec3 operator+(const Vec3& a, const Vec3& b) { return Vec3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline Vec3 operator-(const Vec3& a, const Vec3& b) { return Vec3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline Vec3 operator*(const Vec3& a, const Vec3& b) { return Vec3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline Vec3 operator*(const Vec3& a, double s) { return Vec3(a.x * s, a.y * s, a.z * s); }
+static inline Vec3 operator*(double s, const Vec3& a) { return Vec3(a.x * s, a.y * s, a.z * s); }
+// vec3.rs:171-173 reflect: self - (n * (2.0 * self.dot(n)))
+static inline Vec3 reflect_v(const Vec3& d, const Vec3& n) { return d - n * (2.0 * d.dot(n)); }
+static inline Vec3 vmin(const Vec3& a, const Vec3& b) { return Vec3(std::fmin(a.x, b.x), std::fmin(a.y, b.y), std::fmin(a.z, b.z)); }
+static inline Vec3 vmax(const Vec3& a, const Vec3& b) { return Vec3(std::fmax(a.x, b.x), std::fmax(a.y, b.y), std::fmax(a.z, b.z)); }
+
+// ---------------------------------------------------------------- Color (color.rs) ----
+struct Color {
+    float r = 0, g = 0, b = 0, a = 0;
+    Color() = default;
+    Color(float r_, float g_, float b_, float a_) : r(r_), g(g_), b(b_), a(a_) {}
+    // color.rs:50-58
+    Color gradient(const Color& rhs, double slide) const {
+        double s = std::fmax(slide, 0.0);
+        s = std::fmin(s, 1.0);
+        float a_ = (float)s;
+        float b_ = 1.0f - a_;
+        return Color(r * b_ + rhs.r * a_, g * b_ + rhs.g * a_, b * b_ + rhs.b * a_, 1.0f);
+    }
+};
+// Vec3 * Color (vec3.rs:386-396)
+static inline Vec3 mul_color(const Vec3& v, const Color& c) {
+    return Vec3(v.x * (double)c.r, v.y * (double)c.g, v.z * (double)c.b);
+}
+static inline Vec3 color_to_vec(const Color& c) { return Vec3((double)c.r, (double)c.g, (double)c.b); }
+
+// ---------------------------------------------------------------- Ray (ray.rs) ----
+struct Ray {
+    Vec3 origin, direction;
+    double time = 0;
+    Ray() = default;
+    Ray(const Vec3& o, const Vec3& d, double t) : origin(o), direction(d), time(t) {}
+    // ray.rs:21-31 per-axis mul_add
+    Vec3 at(double t) const {
+        return Vec3(std::fma(direction.x, t, origin.x), std::fma(direction.y, t, origin.y),
+                    std::fma(direction.z, t, origin.z));
+    }
+};
+
+// ---------------------------------------------------------------- FastRng (random.rs:109-145) ----
+// rand_xorshift 0.3.0 XorShiftRng; rand_core 0.6 SeedableRng::seed_from_u64 (PCG32 expansion);
+// next_u64 = lo32 | hi32 << 32 (rand_core impls::next_u64_via_u32).
+struct FastRng {
+    uint32_t x, y, z, w;
+    static FastRng seed_from_u64(uint64_t state) {
+        uint32_t s[4];
+        for (int i = 0; i < 4; ++i) {
+            state = state * 6364136223846793005ULL + 11634580027462260723ULL;
+            uint64_t st = state;
+            uint32_t xorshifted = (uint32_t)(((st >> 18) ^ st) >> 27);
+            uint32_t rot = (uint32_t)(st >> 59);
+            s[i] = (xorshifted >> rot) | (xorshifted << ((32 - rot) & 31));
+        }
+        return from_seed(s);
+    }
+    static FastRng from_seed(const uint32_t s[4]) {
+        FastRng r;
+        if (s[0] == 0 && s[1] == 0 && s[2] == 0 && s[3] == 0) {
+            r.x = r.y = r.z = r.w = 0x0BAD5EED;
+        } else {
+            r.x = s[0]; r.y = s[1]; r.z = s[2]; r.w = s[3];
+        }
+        return r;
+    }
+    uint32_t next_u32() {
+        uint32_t t = x ^ (x << 11);
+        x = y; y = z; z = w;
+        w = w ^ (w >> 19) ^ (t ^ (t >> 8));
+        return w;
+    }
+    uint64_t next_u64() {
+        uint64_t lo = next_u32();
+        uint64_t hi = next_u32();
+        return (hi << 32) | lo;
+    }
+    // random.rs:126 next_u64 as f64 / u64::MAX as f64  (u64::MAX as f64 == 2^64)
+    double gen() { return (double)next_u64() / 18446744073709551616.0; }
+    double range(double a, double b) { return a + gen() * (b - a); }
+    size_t irange(size_t a, size_t b) { return a + (size_t)(next_u32() % (uint32_t)(b - a)); }
+};
+
+static inline uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static inline uint64_t stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
+    uint64_t k = splitmix64(seed);
+    k = splitmix64(k ^ (uint64_t)pass);
+    k = splitmix64(k ^ pixel);
+    k = splitmix64(k ^ (uint64_t)sample);
+    return k;
+}
+
+// vec3.rs:140-147
+static Vec3 random_unit_disk(FastRng& rng) {
+    for (int i = 0; i < RS_REJECTION_CAP; ++i) {
+        double px = rng.range(-1.0, 1.0);
+        double py = rng.range(-1.0, 1.0);
+        Vec3 p(px, py, 0.0);
+        if (p.length_squared() < 1.0) return p;
+    }
+    return Vec3(0, 0, 0);
+}
+// vec3.rs:100-111
+static Vec3 random_cosine_direction(FastRng& rng) {
+    double r1 = rng.gen();
+    double r2 = rng.gen();
+    double q2 = std::sqrt(r2);
+    double phi = 2.0 * PI * r1;
+    return Vec3(std::cos(phi) * q2, std::sin(phi) * q2, std::sqrt(1.0 - r2));
+}
+// vec3.rs:115-126
+static Vec3 random_cosine_direction_exponent(double exponent, FastRng& rng) {
+    double r1 = rng.gen();
+    double r2 = std::pow(rng.gen(), 1.0 / (exponent + 1.0));
+    double sin_theta = std::sqrt(1.0 - r2 * r2);
+    double phi = 2.0 * PI * r1;
+    return Vec3(std::cos(phi) * sin_theta, std::sin(phi) * sin_theta, r2);
+}
+
+// ---------------------------------------------------------------- ONB (onb.rs) ----
+struct ONB {
+    Vec3 axis[3];
+    // onb.rs:14-24 (plain sums, no mul_add)
+    Vec3 local(const Vec3& a) const {
+        const Vec3 &a0 = axis[0], &a1 = axis[1], &a2 = axis[2];
+        return Vec3(a0.x * a.x + a1.x * a.y + a2.x * a.z, a0.y * a.x + a1.y * a.y + a2.y * a.z,
+                    a0.z * a.x + a1.z * a.y + a2.z * a.z);
+    }
+    // onb.rs:26-40
+    static ONB build_from(const Vec3& n) {
+        ONB o;
+        Vec3 w = n.unit();
+        Vec3 up(0.0, 1.0, 0.0);
+        Vec3 uc = up.cross(w);
+        Vec3 u = uc.length_squared() < 0.00000001 ? Vec3(1.0, 0.0, 0.0).cross(w).unit() : uc.unit();
+        Vec3 v = w.cross(u);
+        o.axis[0] = u; o.axis[1] = v; o.axis[2] = w;
+        return o;
+    }
+};
+
+// ---------------------------------------------------------------- PDFs (pdf.rs) ----
+struct Pdf {
+    int kind = 0;  // 0 cosine, 1 reflection
+    ONB onb;          // cosine: about n; reflection: onb_normal
+    ONB onb_reflected;
+    double exponent = 0;
+    double value(const Vec3& d) const {
+        if (kind == 0) {  // pdf.rs:30-36
+            double c = d.dot(onb.axis[2]);
+            return c < 0.0 ? 0.0 : c / PI;
+        }
+        double c = d.dot(onb_reflected.axis[2]);  // pdf.rs:109-116
+        double v = c / PI;
+        return v < 0.0 ? 0.0 : v;
+    }
+    Vec3 generate(FastRng& rng) const {
+        if (kind == 0) return onb.local(random_cosine_direction(rng));  // pdf.rs:39-41
+        for (int i = 0; i < RS_REJECTION_CAP; ++i) {  // pdf.rs:118-134
+            Vec3 d = onb_reflected.local(random_cosine_direction_exponent(exponent, rng));
+            if (d.dot(onb.axis[2]) > 0.0) return d;
+        }
+        return onb.axis[2];
+    }
+    static Pdf cosine(const Vec3& n) { Pdf p; p.kind = 0; p.onb = ONB::build_from(n); return p; }
+    static Pdf reflection(const Vec3& r_in, const Vec3& n, double e) {  // pdf.rs:88-103
+        Pdf p; p.kind = 1; p.exponent = e;
+        Vec3 reflected = reflect_v(r_in, n);
+        p.onb_reflected = ONB::build_from(reflected);
+        p.onb = ONB::build_from(n);
+        return p;
+    }
+};
+
+// ---------------------------------------------------------------- AABB (aabb.rs) ----
+struct AABB {
+    Vec3 min, max;
+    // aabb.rs:20-38
+    bool hit(const Ray& ray, double t_min, double t_max) const {
+        for (int i = 0; i < 3; ++i) {
+            double inv = 1.0 / ray.direction[i];
+            double t0 = (min[i] - ray.origin[i]) * inv;
+            double t1 = (max[i] - ray.origin[i]) * inv;
+            if (inv < 0.0) std::swap(t0, t1);
+            t_min = std::fmax(t_min, t0);
+            t_max = std::fmin(t_max, t1);
+            if (t_max <= t_min) return false;
+        }
+        return true;
+    }
+    AABB operator|(const AABB& o) const { return AABB{vmin(min, o.min), vmax(max, o.max)}; }
+};
+
+// ---------------------------------------------------------------- textures ----
+struct Texture {
+    int kind = RS_TEX_SOLID;
+    Color even, odd;
+    double scale = 1;
+    // checker.rs:21-30
+    Color color(double, double, const Vec3& p) const {
+        if (kind == RS_TEX_SOLID) return even;
+        double value = std::sin(scale * p.x) * std::sin(scale * p.y) * std::sin(scale * p.z);
+        return value < 0.0 ? odd : even;
+    }
+};
+
+// ---------------------------------------------------------------- materials ----
+struct HitRecord;
+struct Material;
+struct ScatterRecord {
+    Color color;
+    bool has_ray = false;
+    Ray ray;
+    Pdf pdf;
+    bool skip_pdf = false;
+};
+
+struct Settings { double phong_factor = 0.0; int32_t phong_exponent = 1; };
+
+struct HitRecord {
+    Vec3 point, normal;
+    const Material* material = nullptr;
+    double t1 = 0, t2 = 0, u = 0, v = 0;
+    bool outside = false;
+};
+
+struct Material {
+    int kind = 0;
+    Texture tex;
+    bool glass = false;
+    double enter_refractive = 1, outer_refractive = 1;
+    double exponent = 0;
+    double multiplier = 1;
+    const Material* m1 = nullptr;
+    const Material* m2 = nullptr;
+    double p1 = 0.5;
+    Settings settings_;
+    int id = -1;
+
+    Settings settings() const { return kind == RS_MAT_MIXED ? m1->settings() : settings_; }
+
+    // light.rs:33-35
+    bool emitted(double u, double v, const Vec3& p, Vec3& out) const {
+        if (kind != RS_MAT_DIFFUSE_LIGHT) return false;
+        out = color_to_vec(tex.color(u, v, p)) * multiplier;
+        return true;
+    }
+
+    // material/mod.rs:75-81 (also metal.rs:14-20)
+    static Ray reflect(const Ray& ray, const HitRecord& hit) {
+        Vec3 rd = ray.direction - (2.0 * ray.direction.dot(hit.normal)) * hit.normal;
+        return Ray(hit.point, rd, ray.time);
+    }
+
+    // dielectric.rs:55-77; Random::normal() -> rng.gen() of the path stream
+    bool refract(const Ray& ray, const HitRecord& hit, FastRng& rng, Ray& out) const {
+        double cos_theta = (-ray.direction).dot(hit.normal);
+        double sin_theta = std::sqrt(1.0 - cos_theta * cos_theta);
+        double refractive = hit.outside ? enter_refractive : outer_refractive;
+        if (refractive * sin_theta > 1.0) return false;
+        double reflect_prob = 0.0;
+        if (glass) {  // dielectric.rs:19-25 Glass::reflect_prob; powi(5) = x*((x*x)*(x*x))
+            double r0 = (1.0 - refractive) / (1.0 + refractive);
+            r0 = r0 * r0;
+            double x = 1.0 - cos_theta;
+            double x2 = x * x;
+            double x5 = x * (x2 * x2);
+            reflect_prob = std::fma(1.0 - r0, x5, r0);
+        }
+        if (rng.gen() < reflect_prob) return false;
+        Vec3 r_parallel = (ray.direction + cos_theta * hit.normal) * refractive;
+        Vec3 r_perp = (-std::sqrt(1.0 - r_parallel.length_squared())) * hit.normal;
+        out = Ray(hit.point, r_parallel + r_perp, ray.time);
+        return true;
+    }
+
+    bool scatter(const Ray& ray, const HitRecord& hit, FastRng& rng, ScatterRecord& s) const {
+        switch (kind) {
+        case RS_MAT_LAMBERTIAN:  // lambertian.rs:39-50
+            s.color = tex.color(hit.u, hit.v, hit.point);
+            s.has_ray = false;
+            s.pdf = Pdf::cosine(hit.normal);
+            s.skip_pdf = false;
+            return true;
+        case RS_MAT_METAL: {  // metal.rs:104-118
+            s.color = tex.color(hit.u, hit.v, hit.point);
+            Ray r = reflect(ray, hit);
+            if (r.direction.dot(hit.normal) > 0.0) {
+                s.has_ray = true; s.ray = r; s.pdf = Pdf::cosine(hit.normal); s.skip_pdf = true;
+                return true;
+            }
+            return false;
+        }
+        case RS_MAT_DIFFUSE_METAL: {  // metal.rs:54-68
+            s.color = tex.color(hit.u, hit.v, hit.point);
+            Ray r = reflect(ray, hit);
+            if (r.direction.dot(hit.normal) > 0.0) {
+                s.has_ray = true; s.ray = r;
+                s.pdf = Pdf::reflection(ray.direction, hit.normal, exponent);
+                s.skip_pdf = false;
+                return true;
+            }
+            return false;
+        }
+        case RS_MAT_DIELECTRIC: {  // dielectric.rs:83-93
+            Ray r;
+            if (!refract(ray, hit, rng, r)) r = reflect(ray, hit);
+            s.color = tex.even;
+            s.has_ray = true; s.ray = r; s.pdf = Pdf::cosine(hit.normal); s.skip_pdf = true;
+            return true;
+        }
+        case RS_MAT_MIXED:  // mixed_material.rs:43-50; thread_rng().next_u32() -> stream
+            if ((double)rng.next_u32() < 4294967295.0 * p1) return m1->scatter(ray, hit, rng, s);
+            return m2->scatter(ray, hit, rng, s);
+        default:  // DiffuseLight: Material::scatter default None (mod.rs:60-62)
+            return false;
+        }
+    }
+};
+
+// ---------------------------------------------------------------- transforms (transform.rs) ----
+typedef double Mat4[4][4];
+static void mat4_id(Mat4 m) {
+    for (int i = 0; i < 4; ++i) for (int j = 0; j < 4; ++j) m[i][j] = i == j ? 1.0 : 0.0;
+}
+// vecmath 1.0.0 mat4_det / mat4_inv (cofactor expansion; restated, see header note)
+static double mat4_det(const Mat4 m) {
+    return m[0][0] * m[1][1] * m[2][2] * m[3][3] + m[0][0] * m[1][2] * m[2][3] * m[3][1] +
+           m[0][0] * m[1][3] * m[2][1] * m[3][2] + m[0][1] * m[1][0] * m[2][3] * m[3][2] +
+           m[0][1] * m[1][2] * m[2][0] * m[3][3] + m[0][1] * m[1][3] * m[2][2] * m[3][0] +
+           m[0][2] * m[1][0] * m[2][1] * m[3][3] + m[0][2] * m[1][1] * m[2][3] * m[3][0] +
+           m[0][2] * m[1][3] * m[2][0] * m[3][1] + m[0][3] * m[1][0] * m[2][2] * m[3][1] +
+           m[0][3] * m[1][1] * m[2][0] * m[3][2] + m[0][3] * m[1][2] * m[2][1] * m[3][0] -
+           m[0][0] * m[1][1] * m[2][3] * m[3][2] - m[0][0] * m[1][2] * m[2][1] * m[3][3] -
+           m[0][0] * m[1][3] * m[2][2] * m[3][1] - m[0][1] * m[1][0] * m[2][2] * m[3][3] -
+           m[0][1] * m[1][2] * m[2][3] * m[3][0] - m[0][1] * m[1][3] * m[2][0] * m[3][2] -
+           m[0][2] * m[1][0] * m[2][3] * m[3][1] - m[0][2] * m[1][1] * m[2][0] * m[3][3] -
+           m[0][2] * m[1][3] * m[2][1] * m[3][0] - m[0][3] * m[1][0] * m[2][1] * m[3][2] -
+           m[0][3] * m[1][1] * m[2][2] * m[3][0] - m[0][3] * m[1][2] * m[2][0] * m[3][1];
+}
+static void mat4_inv(const Mat4 m, Mat4 o) {
+    double inv_det = 1.0 / mat4_det(m);
+    o[0][0] = (m[1][1] * m[2][2] * m[3][3] + m[1][2] * m[2][3] * m[3][1] + m[1][3] * m[2][1] * m[3][2] -
+               m[1][1] * m[2][3] * m[3][2] - m[1][2] * m[2][1] * m[3][3] - m[1][3] * m[2][2] * m[3][1]) * inv_det;
+    o[0][1] = (m[0][1] * m[2][3] * m[3][2] + m[0][2] * m[2][1] * m[3][3] + m[0][3] * m[2][2] * m[3][1] -
+               m[0][1] * m[2][2] * m[3][3] - m[0][2] * m[2][3] * m[3][1] - m[0][3] * m[2][1] * m[3][2]) * inv_det;
+    o[0][2] = (m[0][1] * m[1][2] * m[3][3] + m[0][2] * m[1][3] * m[3][1] + m[0][3] * m[1][1] * m[3][2] -
+               m[0][1] * m[1][3] * m[3][2] - m[0][2] * m[1][1] * m[3][3] - m[0][3] * m[1][2] * m[3][1]) * inv_det;
+    o[0][3] = (m[0][1] * m[1][3] * m[2][2] + m[0][2] * m[1][1] * m[2][3] + m[0][3] * m[1][2] * m[2][1] -
+               m[0][1] * m[1][2] * m[2][3] - m[0][2] * m[1][3] * m[2][1] - m[0][3] * m[1][1] * m[2][2]) * inv_det;
+    o[1][0] = (m[1][0] * m[2][3] * m[3][2] + m[1][2] * m[2][0] * m[3][3] + m[1][3] * m[2][2] * m[3][0] -
+               m[1][0] * m[2][2] * m[3][3] - m[1][2] * m[2][3] * m[3][0] - m[1][3] * m[2][0] * m[3][2]) * inv_det;
+    o[1][1] = (m[0][0] * m[2][2] * m[3][3] + m[0][2] * m[2][3] * m[3][0] + m[0][3] * m[2][0] * m[3][2] -
+               m[0][0] * m[2][3] * m[3][2] - m[0][2] * m[2][0] * m[3][3] - m[0][3] * m[2][2] * m[3][0]) * inv_det;
+    o[1][2] = (m[0][0] * m[1][3] * m[3][2] + m[0][2] * m[1][0] * m[3][3] + m[0][3] * m[1][2] * m[3][0] -
+               m[0][0] * m[1][2] * m[3][3] - m[0][2] * m[1][3] * m[3][0] - m[0][3] * m[1][0] * m[3][2]) * inv_det;
+    o[1][3] = (m[0][0] * m[1][2] * m[2][3] + m[0][2] * m[1][3] * m[2][0] + m[0][3] * m[1][0] * m[2][2] -
+               m[0][0] * m[1][3] * m[2][2] - m[0][2] * m[1][0] * m[2][3] - m[0][3] * m[1][2] * m[2][0]) * inv_det;
+    o[2][0] = (m[1][0] * m[2][1] * m[3][3] + m[1][1] * m[2][3] * m[3][0] + m[1][3] * m[2][0] * m[3][1] -
+               m[1][0] * m[2][3] * m[3][1] - m[1][1] * m[2][0] * m[3][3] - m[1][3] * m[2][1] * m[3][0]) * inv_det;
+    o[2][1] = (m[0][0] * m[2][3] * m[3][1] + m[0][1] * m[2][0] * m[3][3] + m[0][3] * m[2][1] * m[3][0] -
+               m[0][0] * m[2][1] * m[3][3] - m[0][1] * m[2][3] * m[3][0] - m[0][3] * m[2][0] * m[3][1]) * inv_det;
+    o[2][2] = (m[0][0] * m[1][1] * m[3][3] + m[0][1] * m[1][3] * m[3][0] + m[0][3] * m[1][0] * m[3][1] -
+               m[0][0] * m[1][3] * m[3][1] - m[0][1] * m[1][0] * m[3][3] - m[0][3] * m[1][1] * m[3][0]) * inv_det;
+    o[2][3] = (m[0][0] * m[1][3] * m[2][1] + m[0][1] * m[1][0] * m[2][3] + m[0][3] * m[1][1] * m[2][0] -
+               m[0][0] * m[1][1] * m[2][3] - m[0][1] * m[1][3] * m[2][0] - m[0][3] * m[1][0] * m[2][1]) * inv_det;
+    o[3][0] = (m[1][0] * m[2][2] * m[3][1] + m[1][1] * m[2][0] * m[3][2] + m[1][2] * m[2][1] * m[3][0] -
+               m[1][0] * m[2][1] * m[3][2] - m[1][1] * m[2][2] * m[3][0] - m[1][2] * m[2][0] * m[3][1]) * inv_det;
+    o[3][1] = (m[0][0] * m[2][1] * m[3][2] + m[0][1] * m[2][2] * m[3][0] + m[0][2] * m[2][0] * m[3][1] -
+               m[0][0] * m[2][2] * m[3][1] - m[0][1] * m[2][0] * m[3][2] - m[0][2] * m[2][1] * m[3][0]) * inv_det;
+    o[3][2] = (m[0][0] * m[1][2] * m[3][1] + m[0][1] * m[1][0] * m[3][2] + m[0][2] * m[1][1] * m[3][0] -
+               m[0][0] * m[1][1] * m[3][2] - m[0][1] * m[1][2] * m[3][0] - m[0][2] * m[1][0] * m[3][1]) * inv_det;
+    o[3][3] = (m[0][0] * m[1][1] * m[2][2] + m[0][1] * m[1][2] * m[2][0] + m[0][2] * m[1][0] * m[2][1] -
+               m[0][0] * m[1][2] * m[2][1] - m[0][1] * m[1][0] * m[2][2] - m[0][2] * m[1][1] * m[2][0]) * inv_det;
+}
+
+struct Transform { Mat4 matrix; Mat4 inverse; };
+// transform.rs:16-107
+static Transform make_transform(const rs_transform& t) {
+    Transform tf;
+    Mat4& m = tf.matrix;
+    mat4_id(m);
+    switch (t.kind) {
+    case RS_TF_TRANSLATE: m[0][3] = t.v[0]; m[1][3] = t.v[1]; m[2][3] = t.v[2]; break;
+    case RS_TF_ROTATE_X: { double s = std::sin(t.v[0]), c = std::cos(t.v[0]);
+        m[1][1] = c; m[1][2] = s; m[2][1] = -s; m[2][2] = c; break; }
+    case RS_TF_ROTATE_Y: { double s = std::sin(t.v[0]), c = std::cos(t.v[0]);
+        m[0][0] = c; m[0][2] = s; m[2][0] = -s; m[2][2] = c; break; }
+    case RS_TF_ROTATE_Z: { double s = std::sin(t.v[0]), c = std::cos(t.v[0]);
+        m[0][0] = c; m[0][1] = s; m[1][0] = -s; m[1][1] = c; break; }
+    default: m[0][0] = t.v[0]; m[1][1] = t.v[1]; m[2][2] = t.v[2]; m[3][3] = 1.0; break;
+    }
+    mat4_inv(m, tf.inverse);
+    return tf;
+}
+// vecmath row_mat4_transform: r[i] = m[i][0]*v[0] + m[i][1]*v[1] + m[i][2]*v[2] + m[i][3]*v[3]
+static Vec3 mat_apply(const Mat4 m, const Vec3& p, double w) {
+    double r[3];
+    for (int i = 0; i < 3; ++i) r[i] = m[i][0] * p.x + m[i][1] * p.y + m[i][2] * p.z + m[i][3] * w;
+    return Vec3(r[0], r[1], r[2]);
+}
+struct TransformStack {
+    std::vector<Transform> stack;
+    // transform.rs:133-145
+    Vec3 forward(const Vec3& p, double w) const {
+        Vec3 r = p;
+        for (const auto& t : stack) r = mat_apply(t.matrix, r, w);
+        return r;
+    }
+    // transform.rs:147-157
+    Vec3 inverse(const Vec3& p, double w) const {
+        Vec3 r = p;
+        for (auto it = stack.rbegin(); it != stack.rend(); ++it) r = mat_apply(it->inverse, r, w);
+        return r;
+    }
+};
+
+// ---------------------------------------------------------------- hittables ----
+struct Counters { uint64_t segments = 0; };
+
+struct Hittable {
+    virtual ~Hittable() = default;
+    virtual Vec3 normal(const Vec3&) const { return Vec3(0, 1, 0); }
+    virtual const Material* material() const { return nullptr; }
+    virtual void uv(const Vec3&, double& u, double& v) const { u = 0; v = 0; }
+    virtual bool hit(const Ray& r, double tmin, double tmax, HitRecord& rec) const = 0;
+    virtual bool contains(const Vec3& p) const = 0;
+    virtual AABB bbox(double t0, double t1) const = 0;
+    virtual Vec3 random(const Vec3& origin, FastRng& rng) const = 0;
+};
+
+static inline bool range_contains(double t, double a, double b) { return a <= t && t < b; }
+
+// hit.rs:32-53
+static HitRecord make_hit(const Ray& ray, const Hittable& obj, double t1, double t2) {
+    HitRecord h;
+    h.point = ray.at(t1);
+    h.normal = obj.normal(h.point);
+    h.outside = ray.direction.dot(h.normal) < 0.0;
+    if (!h.outside) h.normal = -h.normal;
+    h.material = obj.material();
+    obj.uv(h.point, h.u, h.v);
+    h.t1 = t1; h.t2 = t2;
+    return h;
+}
+// hit.rs:55-67
+static HitRecord with_normal(const Vec3& p, const Vec3& n, const Material* m, double u, double v, double t1, double t2) {
+    HitRecord h;
+    h.point = p; h.normal = n; h.material = m; h.u = u; h.v = v; h.t1 = t1; h.t2 = t2; h.outside = true;
+    return h;
+}
+
+struct Sphere : Hittable {  // sphere.rs
+    Vec3 center, speed;
+    double radius, radius_squared;
+    const Material* mat;
+    Sphere(Vec3 c, double r, Vec3 s, const Material* m) : center(c), speed(s), radius(r), radius_squared(r * r), mat(m) {}
+    Vec3 center_at(double t) const { return center + speed * t; }
+    Vec3 normal(const Vec3& p) const override { return (p - center).div(radius); }
+    const Material* material() const override { return mat; }
+    void uv(const Vec3& point, double& u, double& v) const override {  // sphere.rs:64-71
+        Vec3 p = (point - center).unit();
+        double phi = std::atan2(-p.z, p.x);
+        double theta = std::asin(p.y);
+        u = phi / 2.0 / PI + 0.5;
+        v = theta / PI + 0.5;
+    }
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // sphere.rs:83-109
+        Vec3 cc = center_at(ray.time);
+        Vec3 l = ray.origin - cc;
+        double half_b = ray.direction.dot(l);
+        double a = ray.direction.length_squared();
+        double c = l.length_squared() - radius_squared;
+        double delta = half_b * half_b - a * c;
+        if (delta < 0.0) return false;
+        double sq = std::sqrt(delta);
+        double t1 = (-half_b - sq) / a;
+        double t2 = (-half_b + sq) / a;
+        if (range_contains(t1, tmin, tmax)) { rec = make_hit(ray, *this, t1, t2); return true; }
+        if (range_contains(t2, tmin, tmax)) { rec = make_hit(ray, *this, t2, t2); return true; }
+        return false;
+    }
+    bool contains(const Vec3& p) const override { Vec3 r = center - p; return r.length_squared() < radius * radius; }
+    AABB bbox(double t0, double t1) const override {  // sphere.rs:117-142
+        Vec3 rr(radius, radius, radius);
+        if (speed.x == 0.0 && speed.y == 0.0 && speed.z == 0.0) return AABB{center - rr, center + rr};
+        AABB s{center_at(t0) - rr, center_at(t0) + rr};
+        AABB e{center_at(t1) - rr, center_at(t1) + rr};
+        return s | e;
+    }
+    Vec3 random(const Vec3& origin, FastRng& rng) const override {  // sphere.rs:149-164
+        Vec3 direction = center - origin;
+        ONB uvw = ONB::build_from(direction);
+        for (int i = 0; i < RS_REJECTION_CAP; ++i) {
+            Vec3 u = uvw.axis[0] * rng.gen();
+            Vec3 v = uvw.axis[1] * rng.gen();
+            Vec3 uvv = u + v;
+            if (uvv.length_squared() < 1.0) return (uvv + center) - origin;
+        }
+        return center - origin;
+    }
+};
+
+struct AARect : Hittable {  // rect.rs
+    int ax0, ax1, ax2;
+    double k, a0, a1, b0, b1, a_len, b_len;
+    const Material* mat;
+    AARect(int plane, double k_, double a0_, double a1_, double b0_, double b1_, const Material* m)
+        : k(k_), a0(a0_), a1(a1_), b0(b0_), b1(b1_), a_len(a1_ - a0_), b_len(b1_ - b0_), mat(m) {
+        if (plane == RS_PLANE_XY) { ax0 = 0; ax1 = 1; ax2 = 2; }
+        else if (plane == RS_PLANE_XZ) { ax0 = 0; ax1 = 2; ax2 = 1; }
+        else { ax0 = 1; ax1 = 2; ax2 = 0; }
+    }
+    Vec3 normal(const Vec3&) const override { Vec3 n; n[ax2] = 1.0; return n; }
+    const Material* material() const override { return mat; }
+    void uv(const Vec3& p, double& u, double& v) const override { u = (p[ax0] - a0) / a_len; v = (p[ax1] - b0) / b_len; }
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // rect.rs:101-120
+        double t1 = (k - ray.origin[ax2]) / ray.direction[ax2];
+        if (!range_contains(t1, tmin, tmax)) return false;
+        double a = std::fma(t1, ray.direction[ax0], ray.origin[ax0]);
+        if (a < a0 || a > a1) return false;
+        double b = std::fma(t1, ray.direction[ax1], ray.origin[ax1]);
+        if (b < b0 || b > b1) return false;
+        rec = make_hit(ray, *this, t1, 1.7976931348623157e308);
+        return true;
+    }
+    bool contains(const Vec3&) const override { return false; }
+    AABB bbox(double, double) const override {  // rect.rs:127-139
+        Vec3 p0, p1;
+        p0[ax0] = a0; p0[ax1] = b0; p0[ax2] = k - 0.0001;
+        p1[ax0] = a1; p1[ax1] = b1; p1[ax2] = k + 0.0001;
+        return AABB{p0, p1};
+    }
+    Vec3 random(const Vec3& origin, FastRng& rng) const override {  // rect.rs:141-153
+        Vec3 root(0.0, k, 0.0);
+        root.x = rng.range(a0, a1);
+        root.z = rng.range(b0, b1);
+        return origin - root;
+    }
+};
+
+struct BoxShape : Hittable {  // box.rs
+    Vec3 pmin, pmax;
+    const Material* mat;
+    std::vector<AARect> faces;
+    BoxShape(Vec3 p0, Vec3 p1, const Material* m) : pmin(vmin(p0, p1)), pmax(vmax(p0, p1)), mat(m) {
+        faces.emplace_back(RS_PLANE_XY, pmin.z, pmin.x, pmax.x, pmin.y, pmax.y, m);
+        faces.emplace_back(RS_PLANE_XY, pmax.z, pmin.x, pmax.x, pmin.y, pmax.y, m);
+        faces.emplace_back(RS_PLANE_YZ, pmin.x, pmin.y, pmax.y, pmin.z, pmax.z, m);
+        faces.emplace_back(RS_PLANE_YZ, pmax.x, pmin.y, pmax.y, pmin.z, pmax.z, m);
+        faces.emplace_back(RS_PLANE_XZ, pmin.y, pmin.x, pmax.x, pmin.z, pmax.z, m);
+        faces.emplace_back(RS_PLANE_XZ, pmax.y, pmin.x, pmax.x, pmin.z, pmax.z, m);
+    }
+    Vec3 normal(const Vec3&) const override { return Vec3(0.0, 1.0, 0.0); }
+    const Material* material() const override { return mat; }
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // box.rs:125-149
+        HitRecord hits[6];
+        int n = 0;
+        for (const auto& f : faces) {
+            HitRecord h;
+            if (f.hit(ray, tmin, tmax, h)) hits[n++] = h;
+        }
+        if (n == 1) { rec = hits[0]; return true; }
+        if (n >= 2) {
+            const HitRecord& h1 = hits[0];
+            const HitRecord& h2 = hits[1];
+            if (h1.t1 < h2.t1) rec = with_normal(h1.point, h1.normal, h1.material, h1.u, h1.v, h1.t1, h2.t1);
+            else rec = with_normal(h2.point, h2.normal, h2.material, h2.u, h2.v, h2.t1, h1.t1);
+            return true;
+        }
+        return false;
+    }
+    bool contains(const Vec3& p) const override {
+        return p.x >= pmin.x && p.x <= pmax.x && p.y >= pmin.y && p.y <= pmax.y && p.z >= pmin.z && p.z <= pmax.z;
+    }
+    AABB bbox(double t0, double t1) const override {  // box.rs:155-157 = faces.bbox (list.rs:68-81)
+        AABB r = faces[0].bbox(t0, t1);
+        for (size_t i = 1; i < faces.size(); ++i) r = r | faces[i].bbox(t0, t1);
+        return r;
+    }
+    Vec3 random(const Vec3&, FastRng&) const override { return Vec3(1.0, 0.0, 0.0); }
+};
+
+struct Quadric : Hittable {  // quadric.rs
+    double qa, qb, qc, qd, qe, qf, qg, qh, qi, qj;
+    const Material* mat;
+    Quadric(const double q[10], const Material* m)
+        : qa(q[0]), qb(q[1]), qc(q[2]), qd(q[3]), qe(q[4]), qf(q[5]), qg(q[6]), qh(q[7]), qi(q[8]), qj(q[9]), mat(m) {}
+    Vec3 normal(const Vec3& p) const override {  // quadric.rs:67-100
+        double x = 2.0 * qa * p.x + qb * p.y + qc * p.z + qd;
+        double y = qb * p.x + 2.0 * qe * p.y + qf * p.z + qg;
+        double z = qc * p.x + qf * p.y + 2.0 * qh * p.z + qi;
+        Vec3 r(x, y, z);
+        double len = r.length();
+        if (len == 0.0) return Vec3(1.0, 0.0, 0.0);
+        return r.div(len);
+    }
+    const Material* material() const override { return mat; }
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // quadric.rs:112-182
+        double xo = ray.origin.x, yo = ray.origin.y, zo = ray.origin.z;
+        double xd = ray.direction.x, yd = ray.direction.y, zd = ray.direction.z;
+        double a = xd * (qa * xd + qb * yd + qc * zd) + yd * (qe * yd + qf * zd) + zd * qh * zd;
+        double b = xd * (qa * xo + 0.5 * (qb * yo + qc * zo + qd)) + yd * (qe * yo + 0.5 * (qb * xo + qf * zo + qg)) +
+                   zd * (qh * zo + 0.5 * (qc * xo + qf * yo + qi));
+        double c = xo * (qa * xo + qb * yo + qc * zo + qd) + yo * (qe * yo + qf * zo + qg) + zo * (qh * zo + qi) + qj;
+        if (a == 0.0) {
+            if (b == 0.0) return false;
+            double t1 = -0.5 * c / b;
+            if (range_contains(t1, tmin, tmax)) { rec = make_hit(ray, *this, t1, 1.7976931348623157e308); return true; }
+        } else {
+            double d = b * b - a * c;
+            if (d <= 0.0) return false;
+            double dr = std::sqrt(d);
+            double t1 = (-b - dr) / a;
+            double t2 = (-b + dr) / a;
+            if (range_contains(t1, tmin, tmax)) { rec = make_hit(ray, *this, t1, t2); return true; }
+            if (range_contains(t2, tmin, tmax)) { rec = make_hit(ray, *this, t2, 1.7976931348623157e308); return true; }
+        }
+        return false;
+    }
+    bool contains(const Vec3& p) const override {  // quadric.rs:184-189
+        return (p.x * (qa * p.x + qb * p.y + qd) + p.y * (qe * p.y + qf * p.z + qg) +
+                p.z * (qh * p.z + qc * p.x + qi) + qj) <= 0.0;
+    }
+    AABB bbox(double, double) const override { return AABB{Vec3(-100.0, -100.0, -100.0), Vec3(100.0, 100.0, 100.0)}; }
+    Vec3 random(const Vec3& origin, FastRng&) const override { return -origin; }
+};
+
+struct Triangle : Hittable {  // triangle_mesh.rs:14-160
+    Vec3 p0, n0, n1, n2;
+    double a, b, c, d, e, f;
+    AABB box;
+    const Material* mat;
+    Triangle(Vec3 q0, Vec3 q1, Vec3 q2, const Material* m) : p0(q0), mat(m) {
+        box = AABB{vmin(vmin(q0, q1), q2), vmax(vmax(q0, q1), q2)};
+        a = q0.x - q1.x; b = q0.y - q1.y; c = q0.z - q1.z;
+        d = q0.x - q2.x; e = q0.y - q2.y; f = q0.z - q2.z;
+    }
+    const Material* material() const override { return mat; }
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // :85-131
+        double g = ray.direction.x, h = ray.direction.y, i = ray.direction.z;
+        double j = p0.x - ray.origin.x, k = p0.y - ray.origin.y, l = p0.z - ray.origin.z;
+        double eihf = e * i - h * f;
+        double gfdi = g * f - d * i;
+        double dheg = d * h - e * g;
+        double denom = a * eihf + b * gfdi + c * dheg;
+        double beta = (j * eihf + k * gfdi + l * dheg) / denom;
+        if (beta < 0.0 || beta >= 1.0) return false;
+        double akjb = a * k - j * b;
+        double jcal = j * c - a * l;
+        double blkc = b * l - k * c;
+        double gamma = (i * akjb + h * jcal + g * blkc) / denom;
+        if (gamma <= 0.0 || beta + gamma >= 1.0) return false;
+        double t = -(f * akjb + e * jcal + d * blkc) / denom;
+        if (t >= tmin && t <= tmax) {
+            Vec3 nrm = n0 * (1.0 - beta - gamma) + n1 * beta + n2 * gamma;
+            Vec3 p = ray.at(t);
+            rec = with_normal(p, nrm, mat, 0.0, 0.0, t, 1.7976931348623157e308);
+            return true;
+        }
+        return false;
+    }
+    bool contains(const Vec3&) const override { return false; }
+    AABB bbox(double, double) const override { return box; }
+    Vec3 random(const Vec3& origin, FastRng&) const override { return origin - p0; }
+};
+
+struct Intersection : Hittable {  // csg/intersection.rs
+    std::shared_ptr<Hittable> o1, o2;
+    const Material* mat;
+    Intersection(std::shared_ptr<Hittable> a, std::shared_ptr<Hittable> b, const Material* m) : o1(a), o2(b), mat(m) {}
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // :58-100
+        HitRecord h1, h2;
+        bool ok1 = o1->hit(ray, tmin, tmax, h1);
+        bool ok2 = o2->hit(ray, tmin, tmax, h2);
+        if (ok1 && ok2) {
+            const HitRecord *hits[2];
+            const Hittable *objs[2];
+            if (h1.t1 < h2.t1) { hits[0] = &h1; hits[1] = &h2; objs[0] = o1.get(); objs[1] = o2.get(); }
+            else { hits[0] = &h2; hits[1] = &h1; objs[0] = o2.get(); objs[1] = o1.get(); }
+            if (objs[1]->contains(hits[0]->point)) {
+                rec = *hits[0]; if (!rec.material) rec.material = mat; return true;
+            } else if (objs[0]->contains(hits[1]->point)) {
+                rec = *hits[1]; if (!rec.material) rec.material = mat; return true;
+            }
+        }
+        return false;
+    }
+    bool contains(const Vec3& p) const override { return o1->contains(p) && o2->contains(p); }
+    AABB bbox(double t0, double t1) const override {  // :102-115 (min.z uses b1.min.y upstream)
+        AABB b1 = o1->bbox(t0, t1), b2 = o2->bbox(t0, t1);
+        Vec3 mn(std::fmax(b1.min.x, b2.min.x), std::fmax(b1.min.y, b2.min.y), std::fmax(b1.min.y, b2.min.z));
+        Vec3 mx(std::fmin(b1.max.x, b2.max.x), std::fmin(b1.max.y, b2.max.y), std::fmin(b1.max.z, b2.max.z));
+        return AABB{mn, mx};
+    }
+    Vec3 random(const Vec3& origin, FastRng& rng) const override { return o1->random(origin, rng); }
+};
+
+struct Difference : Hittable {  // csg/difference.rs
+    std::shared_ptr<Hittable> plus, minus;
+    const Material* mat;
+    Difference(std::shared_ptr<Hittable> a, std::shared_ptr<Hittable> b, const Material* m) : plus(a), minus(b), mat(m) {}
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // :57-106
+        HitRecord hp, hm;
+        bool okp = plus->hit(ray, tmin, tmax, hp);
+        bool okm = minus->hit(ray, tmin, tmax, hm);
+        if (okp) {
+            if (okm) {
+                if (hp.t1 < hm.t1) {
+                    if (!minus->contains(hp.point)) { rec = hp; if (!rec.material) rec.material = mat; return true; }
+                } else {
+                    if (hm.t2 < hp.t1) { rec = hp; if (!rec.material) rec.material = mat; return true; }
+                    else if (hm.t2 < hp.t2) {
+                        Vec3 p = ray.at(hm.t2);
+                        Vec3 n = minus->normal(p);
+                        rec = with_normal(p, -n, minus->material(), 0.0, 0.0, hm.t2, hp.t2);
+                        if (!rec.material) rec.material = mat;
+                        return true;
+                    }
+                }
+            } else {
+                rec = hp; return true;
+            }
+        }
+        return false;
+    }
+    bool contains(const Vec3& p) const override { return plus->contains(p) && !minus->contains(p); }
+    AABB bbox(double t0, double t1) const override { return plus->bbox(t0, t1); }
+    Vec3 random(const Vec3& origin, FastRng& rng) const override { return plus->random(origin, rng); }
+};
+
+struct TfFacade : Hittable {  // transform/tf_facade.rs
+    std::shared_ptr<Hittable> object;
+    TransformStack stack;
+    TfFacade(std::shared_ptr<Hittable> o, TransformStack s) : object(o), stack(std::move(s)) {}
+    bool hit(const Ray& rin, double tmin, double tmax, HitRecord& rec) const override {  // :41-55
+        Ray r(stack.inverse(rin.origin, 1.0), stack.inverse(rin.direction, 0.0), rin.time);
+        if (!object->hit(r, tmin, tmax, rec)) return false;
+        rec.point = stack.forward(rec.point, 1.0);
+        return true;
+    }
+    AABB bbox(double t0, double t1) const override {  // :58-90
+        AABB b = object->bbox(t0, t1);
+        Vec3 pmin(INFINITY, INFINITY, INFINITY), pmax(-INFINITY, -INFINITY, -INFINITY);
+        for (int i = 0; i < 2; ++i) for (int j = 0; j < 2; ++j) for (int k = 0; k < 2; ++k) {
+            double x = std::fma((double)i, b.max.x, (double)(1 - i) * b.min.x);
+            double y = std::fma((double)j, b.max.y, (double)(1 - j) * b.min.y);
+            double z = std::fma((double)k, b.max.z, (double)(1 - k) * b.min.z);
+            Vec3 tp = stack.forward(Vec3(x, y, z), 1.0);
+            for (int c = 0; c < 3; ++c) { pmin[c] = std::fmin(pmin[c], tp[c]); pmax[c] = std::fmax(pmax[c], tp[c]); }
+        }
+        return AABB{pmin, pmax};
+    }
+    bool contains(const Vec3& p) const override { return object->contains(stack.inverse(p, 1.0)); }
+    Vec3 random(const Vec3& origin, FastRng& rng) const override { return object->random(stack.inverse(origin, 1.0), rng); }
+};
+
+// bvh.rs:47-113 (deterministic axis, one object per leaf: see header)
+struct BVHNode {
+    AABB box;
+    int left = -1, right = -1;  // child node indices
+    const Hittable* obj = nullptr;  // leaf
+};
+struct BVH {
+    std::vector<BVHNode> nodes;
+    int root = -1;
+    void build(std::vector<std::pair<const Hittable*, AABB>>& objs, double t0, double t1) {
+        nodes.clear();
+        if (objs.empty()) { root = -1; return; }
+        std::vector<std::pair<const Hittable*, std::pair<AABB, AABB>>> items;  // (obj, (sortbox, box))
+        for (auto& o : objs) items.push_back({o.first, {o.first->bbox(0.0, 0.0), o.second}});
+        (void)t0; (void)t1;
+        root = build_rec(items, 0, items.size());
+    }
+    int build_rec(std::vector<std::pair<const Hittable*, std::pair<AABB, AABB>>>& it, size_t b, size_t e) {
+        int idx = (int)nodes.size();
+        nodes.emplace_back();
+        if (e - b == 1) {
+            nodes[idx].box = it[b].second.second;
+            nodes[idx].obj = it[b].first;
+            return idx;
+        }
+        // find_best_axis (bvh.rs:116-169) over the node's objects
+        AABB u = it[b].second.second;
+        for (size_t i = b + 1; i < e; ++i) u = u | it[i].second.second;
+        Vec3 size = u.max - u.min;
+        int axis = 0;
+        if (size.x > size.y && size.x > size.z) axis = 0;
+        else if (size.y > size.x && size.y > size.z) axis = 1;
+        else if (size.z > size.x && size.z > size.y) axis = 2;
+        std::stable_sort(it.begin() + b, it.begin() + e, [axis](const auto& p, const auto& q) {
+            return p.second.first.min[axis] < q.second.first.min[axis];
+        });
+        size_t mid = b + (e - b) / 2;
+        int l = build_rec(it, b, mid);
+        int r = build_rec(it, mid, e);
+        nodes[idx].left = l; nodes[idx].right = r;
+        nodes[idx].box = nodes[l].box | nodes[r].box;
+        return idx;
+    }
+    // bvh.rs:173-192
+    bool hit(int n, const Ray& ray, double tmin, double tmax, HitRecord& rec) const {
+        const BVHNode& node = nodes[n];
+        if (!node.box.hit(ray, tmin, tmax)) return false;
+        if (node.obj) return node.obj->hit(ray, tmin, tmax, rec);
+        HitRecord hl;
+        bool okl = hit(node.left, ray, tmin, tmax, hl);
+        HitRecord hr;
+        bool okr = hit(node.right, ray, tmin, okl ? hl.t1 : tmax, hr);
+        if (okr) { rec = hr; return true; }
+        if (okl) { rec = hl; return true; }
+        return false;
+    }
+};
+
+// ---------------------------------------------------------------- world + camera ----
+struct Scene {
+    std::vector<std::unique_ptr<Material>> materials;
+    std::vector<std::shared_ptr<Hittable>> handles;
+    std::vector<uint32_t> world, lights;
+    Color bg_lo{0.3f, 0.4f, 0.5f, 1.0f}, bg_hi{0.7f, 0.89f, 1.0f, 1.0f};
+    Material default_material;  // world.rs:51 Lambertian(Color(1,1,1,1))
+    BVH bvh;
+    bool committed = false;
+    double time0 = 0, time1 = 0;
+    Scene() {
+        default_material.kind = RS_MAT_LAMBERTIAN;
+        default_material.tex.kind = RS_TEX_SOLID;
+        default_material.tex.even = Color(1, 1, 1, 1);
+    }
+    const Material* mat(int32_t id) const {
+        if (id < 0 || (size_t)id >= materials.size()) return nullptr;
+        return materials[id].get();
+    }
+    bool world_hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const {
+        if (bvh.root < 0) return false;
+        return bvh.hit(bvh.root, ray, tmin, tmax, rec);
+    }
+    // list.rs:49-52
+    Vec3 lights_random(const Vec3& origin, FastRng& rng) const {
+        size_t i = rng.irange(0, lights.size());
+        return handles[lights[i]]->random(origin, rng);
+    }
+    Color background(const Ray& ray) const {  // rtow_13_1.rs:38-41 / raysnail.rs:364-367
+        double t = (ray.direction.y + 1.0) * 0.5;
+        return bg_lo.gradient(bg_hi, t);
+    }
+};
+
+struct Camera {  // camera.rs:18-85
+    Vec3 origin, lb, horizontal_full, vertical_full, horizontal_unit, vertical_unit;
+    double aperture, shutter;
+    uint32_t width, height;
+    explicit Camera(const rs_camera_desc& d) {
+        Vec3 look_from(d.look_from[0], d.look_from[1], d.look_from[2]);
+        Vec3 look_at(d.look_at[0], d.look_at[1], d.look_at[2]);
+        Vec3 vup(d.vup[0], d.vup[1], d.vup[2]);
+        double aspect = (double)d.width / (double)d.height;  // camera.rs:384-397
+        double theta = d.fov * (PI / 180.0);                 // f64::to_radians
+        double h = std::tan(theta / 2.0);
+        double vh = 2.0 * h * d.focus;
+        double vw = vh * aspect;
+        Vec3 w = (look_at - look_from).unit();
+        horizontal_unit = w.cross(vup).unit();
+        vertical_unit = horizontal_unit.cross(w).unit();
+        horizontal_full = vw * horizontal_unit;
+        vertical_full = vh * vertical_unit;
+        lb = look_from - horizontal_full.div(2.0) - vertical_full.div(2.0) + d.focus * w;
+        origin = look_from;
+        aperture = d.aperture; shutter = d.shutter; width = d.width; height = d.height;
+    }
+    Ray ray(double u, double v, FastRng& rng) const {  // camera.rs:77-85
+        Vec3 rd = (aperture / 2.0) * random_unit_disk(rng);
+        Vec3 offset = horizontal_unit * rd.x + vertical_unit * rd.y;
+        Vec3 o = origin + offset;
+        Vec3 dir = lb + u * horizontal_full + v * vertical_full - o;
+        return Ray(o, dir.unit(), shutter * rng.gen());
+    }
+};
+
+// compiler-rt __powidf2 (runtime-exponent powi)
+static double powi_rt(double a, int b) {
+    const int recip = b < 0;
+    double r = 1;
+    while (1) {
+        if (b & 1) r *= a;
+        b /= 2;
+        if (b == 0) break;
+        a *= a;
+    }
+    return recip ? 1 / r : r;
+}
+// camera.rs:94-100
+static double phong_highlight(const Vec3& dir_to_light, const Vec3& ray_dir, const Vec3& normal, int exponent, double factor) {
+    Vec3 reflected = dir_to_light - (2.0 * dir_to_light.dot(normal)) * normal;
+    double spec = powi_rt(std::fmax(reflected.dot(-ray_dir), 0.0), exponent);
+    return spec * factor;
+}
+
+// camera.rs:156-255
+static Vec3 ray_color(const Scene& sc, const Ray& ray, uint32_t depth, FastRng& rng, Counters& cnt) {
+    if (depth == 0) return Vec3();
+    HitRecord hit;
+    cnt.segments++;
+    if (sc.world_hit(ray, 0.0001, INFINITY, hit)) {
+        const Material* material = hit.material ? hit.material : &sc.default_material;
+        Vec3 emitted;
+        material->emitted(hit.u, hit.v, hit.point, emitted);
+        ScatterRecord srec;
+        if (material->scatter(ray, hit, rng, srec)) {
+            if (srec.skip_pdf) {
+                if (srec.has_ray) return emitted + mul_color(ray_color(sc, srec.ray, depth - 1, rng, cnt), srec.color);
+                return emitted + mul_color(Vec3(1.0, 1.0, 1.0), srec.color);
+            }
+            double light_multi = 1.0;
+            double pdf_val;
+            Ray scattered;
+            if (rng.gen() < 0.5) {
+                pdf_val = 0.3183098861837907;
+                Vec3 dir_to_light = sc.lights_random(hit.point, rng).unit();
+                Settings st = material->settings();
+                if (st.phong_factor > 0.0)
+                    light_multi += phong_highlight(-dir_to_light, ray.direction, hit.normal, st.phong_exponent, st.phong_factor);
+                Vec3 start = ray.at(hit.t1 - 0.0002);
+                scattered = Ray(start, dir_to_light, ray.time);
+            } else {
+                Vec3 sd = srec.pdf.generate(rng);
+                pdf_val = srec.pdf.value(sd);
+                scattered = Ray(hit.point, sd, ray.time);
+            }
+            if (pdf_val <= 0.0 || pdf_val != pdf_val) pdf_val = 1e-5;
+            double spv = srec.pdf.value(scattered.direction);
+            double mult = spv / pdf_val;
+            Vec3 sample_color = light_multi * ray_color(sc, scattered, depth - 1, rng, cnt);
+            Vec3 cfs = mul_color(sample_color, srec.color) * mult;
+            return emitted + cfs;
+        }
+        return emitted;
+    }
+    return color_to_vec(sc.background(ray));
+}
+
+}  // namespace orc
+
+// ======================================================================== C API ====
+using namespace orc;
+
+struct orc_scene { Scene s; };
+
+extern "C" {
+
+static thread_local std::string g_err;
+static int fail(int code, const char* msg) { g_err = msg; return code; }
+
+const char* orc_last_error(void) { return g_err.c_str(); }
+uint64_t orc_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
+    return stream_key(seed, pass, pixel, sample);
+}
+
+orc_scene* orc_scene_create(void) { return new orc_scene(); }
+void orc_scene_destroy(orc_scene* s) { delete s; }
+
+int orc_material(orc_scene* s, const rs_material_desc* d, int32_t* id_out) {
+    if (!s || !d) return fail(RS_E_INVALID, "null argument");
+    auto m = std::make_unique<Material>();
+    m->kind = d->kind;
+    m->tex.kind = d->texture.kind;
+    m->tex.even = Color(d->texture.even[0], d->texture.even[1], d->texture.even[2], d->texture.even[3]);
+    m->tex.odd = Color(d->texture.odd[0], d->texture.odd[1], d->texture.odd[2], d->texture.odd[3]);
+    m->tex.scale = d->texture.scale;
+    m->glass = d->glass != 0;
+    m->enter_refractive = 1.0 / d->refractive;  // dielectric.rs:35-41
+    m->outer_refractive = d->refractive;
+    m->exponent = d->exponent;
+    m->multiplier = d->multiplier;
+    m->p1 = d->mix_p;
+    m->settings_.phong_factor = d->phong_factor;
+    m->settings_.phong_exponent = d->phong_exponent;
+    if (d->kind == RS_MAT_MIXED) {
+        m->m1 = s->s.mat(d->mix_a);
+        m->m2 = s->s.mat(d->mix_b);
+        if (!m->m1 || !m->m2) return fail(RS_E_INVALID, "mixed material refers to unknown ids");
+    }
+    if (d->kind < 0 || d->kind > RS_MAT_MIXED) return fail(RS_E_INVALID, "unknown material kind");
+    m->id = (int)s->s.materials.size();
+    *id_out = m->id;
+    s->s.materials.push_back(std::move(m));
+    return RS_OK;
+}
+
+static int push_handle(orc_scene* s, std::shared_ptr<Hittable> h, uint32_t* out) {
+    *out = (uint32_t)s->s.handles.size();
+    s->s.handles.push_back(std::move(h));
+    return RS_OK;
+}
+
+int orc_sphere(orc_scene* s, const double c[3], double r, const double speed[3], int32_t mat, uint32_t* out) {
+    Vec3 sp = speed ? Vec3(speed[0], speed[1], speed[2]) : Vec3();
+    return push_handle(s, std::make_shared<Sphere>(Vec3(c[0], c[1], c[2]), r, sp, s->s.mat(mat)), out);
+}
+int orc_aarect(orc_scene* s, int32_t plane, double k, double a0, double a1, double b0, double b1, int32_t mat, uint32_t* out) {
+    if (plane < 0 || plane > 2) return fail(RS_E_INVALID, "bad plane");
+    return push_handle(s, std::make_shared<AARect>(plane, k, a0, a1, b0, b1, s->s.mat(mat)), out);
+}
+int orc_box(orc_scene* s, const double p0[3], const double p1[3], int32_t mat, uint32_t* out) {
+    return push_handle(s, std::make_shared<BoxShape>(Vec3(p0[0], p0[1], p0[2]), Vec3(p1[0], p1[1], p1[2]), s->s.mat(mat)), out);
+}
+int orc_quadric(orc_scene* s, const double q[10], int32_t mat, uint32_t* out) {
+    return push_handle(s, std::make_shared<Quadric>(q, s->s.mat(mat)), out);
+}
+int orc_triangles(orc_scene* s, const double* pos, const double* nrm, uint32_t n, int32_t mat, uint32_t* first) {
+    *first = (uint32_t)s->s.handles.size();
+    for (uint32_t i = 0; i < n; ++i) {
+        const double* p = pos + 9 * i;
+        auto t = std::make_shared<Triangle>(Vec3(p[0], p[1], p[2]), Vec3(p[3], p[4], p[5]), Vec3(p[6], p[7], p[8]), s->s.mat(mat));
+        if (nrm) {
+            const double* q = nrm + 9 * i;
+            t->n0 = Vec3(q[0], q[1], q[2]); t->n1 = Vec3(q[3], q[4], q[5]); t->n2 = Vec3(q[6], q[7], q[8]);
+        }
+        s->s.handles.push_back(t);
+    }
+    return RS_OK;
+}
+int orc_intersection(orc_scene* s, uint32_t a, uint32_t b, int32_t mat, uint32_t* out) {
+    if (a >= s->s.handles.size() || b >= s->s.handles.size()) return fail(RS_E_INVALID, "bad handle");
+    return push_handle(s, std::make_shared<Intersection>(s->s.handles[a], s->s.handles[b], s->s.mat(mat)), out);
+}
+int orc_difference(orc_scene* s, uint32_t a, uint32_t b, int32_t mat, uint32_t* out) {
+    if (a >= s->s.handles.size() || b >= s->s.handles.size()) return fail(RS_E_INVALID, "bad handle");
+    return push_handle(s, std::make_shared<Difference>(s->s.handles[a], s->s.handles[b], s->s.mat(mat)), out);
+}
+int orc_transformed(orc_scene* s, uint32_t obj, const rs_transform* st, uint32_t n, uint32_t* out) {
+    if (obj >= s->s.handles.size()) return fail(RS_E_INVALID, "bad handle");
+    TransformStack ts;
+    for (uint32_t i = 0; i < n; ++i) ts.stack.push_back(make_transform(st[i]));
+    return push_handle(s, std::make_shared<TfFacade>(s->s.handles[obj], ts), out);
+}
+int orc_world_add(orc_scene* s, uint32_t h) {
+    if (h >= s->s.handles.size()) return fail(RS_E_INVALID, "bad handle");
+    s->s.world.push_back(h); return RS_OK;
+}
+int orc_lights_add(orc_scene* s, uint32_t h) {
+    if (h >= s->s.handles.size()) return fail(RS_E_INVALID, "bad handle");
+    s->s.lights.push_back(h); return RS_OK;
+}
+int orc_set_background(orc_scene* s, const float lo[3], const float hi[3]) {
+    s->s.bg_lo = Color(lo[0], lo[1], lo[2], 1.0f);
+    s->s.bg_hi = Color(hi[0], hi[1], hi[2], 1.0f);
+    return RS_OK;
+}
+int orc_set_time_range(orc_scene* s, double t0, double t1) {
+    s->s.time0 = t0; s->s.time1 = t1; return RS_OK;
+}
+int orc_commit(orc_scene* s) {
+    std::vector<std::pair<const Hittable*, AABB>> objs;
+    for (uint32_t h : s->s.world) {
+        const Hittable* o = s->s.handles[h].get();
+        objs.push_back({o, o->bbox(s->s.time0, s->s.time1)});
+    }
+    s->s.bvh.build(objs, s->s.time0, s->s.time1);
+    s->s.committed = true;
+    return RS_OK;
+}
+
+// Painter::draw restated: T threads, thread i renders rows i, i+T, ... of the requested lattice
+// (painter.rs:239-299), render_pixel per pixel (painter.rs:154-187).
+int orc_render(orc_scene* s, const rs_camera_desc* cd, const rs_render_settings* st, const uint8_t* mask,
+               float* out, int threads, rs_render_stats* stats) {
+    if (!s || !cd || !st || !out) return fail(RS_E_INVALID, "null argument");
+    if (!s->s.committed) return fail(RS_E_STATE, "scene not committed");
+    if (cd->width == 0 || cd->height == 0) return fail(RS_E_INVALID, "empty image");
+    Camera cam(*cd);
+    const Scene& sc = s->s;
+    uint32_t sqrt_spp = (uint32_t)std::floor(std::sqrt((double)st->samples));  // painter.rs:110-118
+    uint32_t nsamp = sqrt_spp * sqrt_spp;
+    uint32_t W = cd->width, H = cd->height;
+    uint32_t rb = st->row_begin, re = st->row_end ? std::min(st->row_end, H) : H;
+    uint32_t rs = st->row_step ? st->row_step : 1;
+    std::vector<uint32_t> rows;
+    for (uint32_t y = rb; y < re; y += rs) rows.push_back(y);
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency() + 1;  // painter.rs:321-325
+    std::atomic<uint64_t> seg_total{0}, samp_total{0};
+    auto worker = [&](int ti) {
+        Counters cnt;
+        uint64_t samples = 0;
+        for (size_t ri = (size_t)ti; ri < rows.size(); ri += (size_t)threads) {
+            uint32_t y = rows[ri];
+            for (uint32_t x = 0; x < W; ++x) {
+                float* o = out + 4 * ((size_t)y * W + x);
+                size_t pix = (size_t)y * W + x;
+                if (mask && !mask[pix]) { o[0] = o[1] = o[2] = o[3] = 0.0f; continue; }
+                Vec3 cv(0, 0, 0);
+                double xf = (double)x, yf = (double)y;
+                for (uint32_t sj = 0; sj < sqrt_spp; ++sj) {
+                    for (uint32_t si = 0; si < sqrt_spp; ++si) {
+                        FastRng rng = FastRng::seed_from_u64(stream_key(st->seed, st->pass, pix, sj * sqrt_spp + si));
+                        double xo = xf + ((double)si + rng.gen()) / (double)sqrt_spp;
+                        double yo = yf + ((double)sj + rng.gen()) / (double)sqrt_spp;
+                        double hgt = (double)H;
+                        double u = xo / (double)W;                    // painter.rs:133-139
+                        double v = (hgt - 1.0 - yo) / hgt;
+                        Ray r = cam.ray(u, v, rng);
+                        Vec3 c = ray_color(sc, r, st->depth, rng, cnt);
+                        cv = cv + c;
+                        ++samples;
+                    }
+                }
+                // vec3.rs:227-240 into_color: DivAssign (true division), sqrt, as f32
+                double n = (double)nsamp;
+                double cx = cv.x / n, cy = cv.y / n, cz = cv.z / n;
+                if (st->gamma) { cx = std::sqrt(cx); cy = std::sqrt(cy); cz = std::sqrt(cz); }
+                o[0] = (float)cx; o[1] = (float)cy; o[2] = (float)cz; o[3] = 1.0f;
+            }
+        }
+        seg_total += cnt.segments;
+        samp_total += samples;
+    };
+    std::vector<std::thread> pool;
+    for (int i = 0; i < threads; ++i) pool.emplace_back(worker, i);
+    for (auto& t : pool) t.join();
+    if (stats) { stats->segments = seg_total.load(); stats->samples = samp_total.load(); stats->ms = 0; }
+    return RS_OK;
+}
+
+// Radiance of ONE camera sample (before into_color): for per-sample parity probes.
+int orc_sample_radiance(orc_scene* s, const rs_camera_desc* cd, const rs_render_settings* st, uint32_t x, uint32_t y,
+                        uint32_t sample, double out[3], uint64_t* segments) {
+    if (!s->s.committed) return fail(RS_E_STATE, "scene not committed");
+    Camera cam(*cd);
+    uint32_t sqrt_spp = (uint32_t)std::floor(std::sqrt((double)st->samples));
+    uint32_t sj = sample / sqrt_spp, si = sample % sqrt_spp;
+    size_t pix = (size_t)y * cd->width + x;
+    FastRng rng = FastRng::seed_from_u64(stream_key(st->seed, st->pass, pix, sample));
+    double xo = (double)x + ((double)si + rng.gen()) / (double)sqrt_spp;
+    double yo = (double)y + ((double)sj + rng.gen()) / (double)sqrt_spp;
+    double hgt = (double)cd->height;
+    Ray r = cam.ray(xo / (double)cd->width, (hgt - 1.0 - yo) / hgt, rng);
+    Counters cnt;
+    Vec3 c = ray_color(s->s, r, st->depth, rng, cnt);
+    out[0] = c.x; out[1] = c.y; out[2] = c.z;
+    if (segments) *segments = cnt.segments;
+    return RS_OK;
+}
+
+// ---- KAT probes (tests/test_oracle_kat.py) ----
+void orc_rng_u32(uint64_t seed, uint32_t n, uint32_t* out) {
+    FastRng r = FastRng::seed_from_u64(seed);
+    for (uint32_t i = 0; i < n; ++i) out[i] = r.next_u32();
+}
+void orc_rng_u32_from_words(const uint32_t s[4], uint32_t n, uint32_t* out) {
+    FastRng r = FastRng::from_seed(s);
+    for (uint32_t i = 0; i < n; ++i) out[i] = r.next_u32();
+}
+void orc_rng_gen(uint64_t seed, uint32_t n, double* out) {
+    FastRng r = FastRng::seed_from_u64(seed);
+    for (uint32_t i = 0; i < n; ++i) out[i] = r.gen();
+}
+// world.hit probe: out = [hit, t1, t2, px, py, pz, nx, ny, nz, u, v, outside, material_id]
+int orc_world_hit(orc_scene* s, const double o[3], const double d[3], double time, double tmin, double tmax, double out[13]) {
+    if (!s->s.committed) return fail(RS_E_STATE, "scene not committed");
+    Ray r(Vec3(o[0], o[1], o[2]), Vec3(d[0], d[1], d[2]), time);
+    HitRecord h;
+    bool ok = s->s.world_hit(r, tmin, tmax, h);
+    std::memset(out, 0, sizeof(double) * 13);
+    out[0] = ok ? 1.0 : 0.0;
+    if (ok) {
+        out[1] = h.t1; out[2] = h.t2; out[3] = h.point.x; out[4] = h.point.y; out[5] = h.point.z;
+        out[6] = h.normal.x; out[7] = h.normal.y; out[8] = h.normal.z; out[9] = h.u; out[10] = h.v;
+        out[11] = h.outside ? 1.0 : 0.0; out[12] = h.material ? (double)h.material->id : -1.0;
+    }
+    return RS_OK;
+}
+// TransformStack probe (transform.rs:133-157; KAT of the reference's own test_y_rotation :187-206)
+void orc_tf_apply(const rs_transform* st, uint32_t n, const double p[3], double w, int inverse, double out[3]) {
+    TransformStack ts;
+    for (uint32_t i = 0; i < n; ++i) ts.stack.push_back(make_transform(st[i]));
+    Vec3 r = inverse ? ts.inverse(Vec3(p[0], p[1], p[2]), w) : ts.forward(Vec3(p[0], p[1], p[2]), w);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+// Camera::ray probe: out = [ox, oy, oz, dx, dy, dz, time]
+void orc_camera_ray(const rs_camera_desc* cd, double u, double v, uint64_t rng_seed, double out[7]) {
+    Camera cam(*cd);
+    FastRng rng = FastRng::seed_from_u64(rng_seed);
+    Ray r = cam.ray(u, v, rng);
+    out[0] = r.origin.x; out[1] = r.origin.y; out[2] = r.origin.z;
+    out[3] = r.direction.x; out[4] = r.direction.y; out[5] = r.direction.z; out[6] = r.time;
+}
+// Material::scatter probe on a synthetic hit. in: ray o,d,time; hit p,n,t1,outside. out:
+// [ok, skip, has_ray, cr, cg, cb, rox, roy, roz, rdx, rdy, rdz, pdf_dir_x, pdf_dir_y, pdf_dir_z, pdf_value]
+int orc_scatter(orc_scene* s, int32_t mat, const double ray_in[7], const double hit_in[8], uint64_t rng_seed, double out[16]) {
+    const Material* m = s->s.mat(mat);
+    if (!m) return fail(RS_E_INVALID, "bad material");
+    Ray r(Vec3(ray_in[0], ray_in[1], ray_in[2]), Vec3(ray_in[3], ray_in[4], ray_in[5]), ray_in[6]);
+    HitRecord h;
+    h.point = Vec3(hit_in[0], hit_in[1], hit_in[2]);
+    h.normal = Vec3(hit_in[3], hit_in[4], hit_in[5]);
+    h.t1 = hit_in[6]; h.outside = hit_in[7] != 0.0;
+    h.material = m;
+    FastRng rng = FastRng::seed_from_u64(rng_seed);
+    ScatterRecord sr;
+    std::memset(out, 0, sizeof(double) * 16);
+    bool ok = m->scatter(r, h, rng, sr);
+    out[0] = ok;
+    if (!ok) return RS_OK;
+    out[1] = sr.skip_pdf; out[2] = sr.has_ray;
+    out[3] = sr.color.r; out[4] = sr.color.g; out[5] = sr.color.b;
+    out[6] = sr.ray.origin.x; out[7] = sr.ray.origin.y; out[8] = sr.ray.origin.z;
+    out[9] = sr.ray.direction.x; out[10] = sr.ray.direction.y; out[11] = sr.ray.direction.z;
+    Vec3 g = sr.pdf.generate(rng);
+    out[12] = g.x; out[13] = g.y; out[14] = g.z;
+    out[15] = sr.pdf.value(g);
+    return RS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,911 @@
+// rs_host.cpp — host half of libraysnail_hip.so: the C-ABI (include/raysnail_hip.h), scene
+// flattening into the device layout (rs_layout.h), bounding boxes, BVH build, upload and the
+// render orchestration (batches of camera samples -> ordered accumulation -> into_color).
+//
+// Reference behaviour restated here (host side, once per scene / frame):
+//   bounding boxes        sphere.rs:117-142, rect.rs:127-139, box.rs:155-157 (faces list.rs:68-81),
+//                         quadric.rs:191-196, triangle_mesh.rs:133-135, intersection.rs:102-115
+//                         (min.z from b1.min.y, kept), difference.rs:109-111, tf_facade.rs:58-90
+//   transforms            transform.rs:16-107 (+ vecmath 1.0.0 mat4_inv)
+//   Camera::new           camera.rs:37-73, CameraBuilder width/height aspect camera.rs:384-397
+//   Painter::samples      painter.rs:110-118 (N = floor(sqrt(requested))^2)
+// The BVH is this library's own (binned SAH, one object per leaf); BVH topology is not a parity
+// obligation because every leaf box is the object's own bbox.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <functional>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/raysnail_hip.h"
+#include "rs_internal.h"
+#include "rs_layout.h"
+
+using namespace rs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_OK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t e_ = (x);                                                                               \
+        if (e_ != hipSuccess) throw Error(RS_E_HIP, std::string(#x " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Box3 {
+    double lo[3], hi[3];
+};
+Box3 box_union(const Box3& a, const Box3& b) {
+    Box3 r;
+    for (int i = 0; i < 3; ++i) { r.lo[i] = std::fmin(a.lo[i], b.lo[i]); r.hi[i] = std::fmax(a.hi[i], b.hi[i]); }
+    return r;
+}
+Box3 box_empty() {
+    Box3 r;
+    for (int i = 0; i < 3; ++i) { r.lo[i] = INFINITY; r.hi[i] = -INFINITY; }
+    return r;
+}
+
+// host object record, one per handle
+struct HObj {
+    int32_t kind = 0;
+    int32_t mat = RS_NO_MATERIAL;
+    double p[18] = {0};
+    int32_t a = -1, b = -1;            // children (CSG / XFORM child in a)
+    int32_t ax[3] = {0, 0, 0};         // rect axes
+    std::vector<rs_transform> tfs;     // XFORM
+};
+
+typedef double M4[4][4];
+
+// vecmath 1.0.0 mat4_det / mat4_inv: explicit cofactor expansion, 1/det scaling.
+double det4(const M4 m) {
+    double pos = m[0][0] * m[1][1] * m[2][2] * m[3][3] + m[0][0] * m[1][2] * m[2][3] * m[3][1] +
+                 m[0][0] * m[1][3] * m[2][1] * m[3][2] + m[0][1] * m[1][0] * m[2][3] * m[3][2] +
+                 m[0][1] * m[1][2] * m[2][0] * m[3][3] + m[0][1] * m[1][3] * m[2][2] * m[3][0] +
+                 m[0][2] * m[1][0] * m[2][1] * m[3][3] + m[0][2] * m[1][1] * m[2][3] * m[3][0] +
+                 m[0][2] * m[1][3] * m[2][0] * m[3][1] + m[0][3] * m[1][0] * m[2][2] * m[3][1] +
+                 m[0][3] * m[1][1] * m[2][0] * m[3][2] + m[0][3] * m[1][2] * m[2][1] * m[3][0];
+    return pos - m[0][0] * m[1][1] * m[2][3] * m[3][2] - m[0][0] * m[1][2] * m[2][1] * m[3][3] -
+           m[0][0] * m[1][3] * m[2][2] * m[3][1] - m[0][1] * m[1][0] * m[2][2] * m[3][3] -
+           m[0][1] * m[1][2] * m[2][3] * m[3][0] - m[0][1] * m[1][3] * m[2][0] * m[3][2] -
+           m[0][2] * m[1][0] * m[2][3] * m[3][1] - m[0][2] * m[1][1] * m[2][0] * m[3][3] -
+           m[0][2] * m[1][3] * m[2][1] * m[3][0] - m[0][3] * m[1][0] * m[2][1] * m[3][2] -
+           m[0][3] * m[1][1] * m[2][2] * m[3][0] - m[0][3] * m[1][2] * m[2][0] * m[3][1];
+}
+// cofactor term: sum of three "+" triple products minus three "-" ones, as vecmath writes them
+double cof(const M4 m, int a0, int a1, int b0, int b1, int c0, int c1, int d0, int d1, int e0, int e1, int f0, int f1,
+           int g0, int g1, int h0, int h1, int i0, int i1, int j0, int j1, int k0, int k1, int l0, int l1,
+           int mm0, int mm1, int n0, int n1, int o0, int o1, int q0, int q1, int r0, int r1, int s0, int s1) {
+    return m[a0][a1] * m[b0][b1] * m[c0][c1] + m[d0][d1] * m[e0][e1] * m[f0][f1] + m[g0][g1] * m[h0][h1] * m[i0][i1] -
+           m[j0][j1] * m[k0][k1] * m[l0][l1] - m[mm0][mm1] * m[n0][n1] * m[o0][o1] - m[q0][q1] * m[r0][r1] * m[s0][s1];
+}
+void inv4(const M4 m, M4 o) {
+    const double id = 1.0 / det4(m);
+    o[0][0] = cof(m, 1,1,2,2,3,3, 1,2,2,3,3,1, 1,3,2,1,3,2, 1,1,2,3,3,2, 1,2,2,1,3,3, 1,3,2,2,3,1) * id;
+    o[0][1] = cof(m, 0,1,2,3,3,2, 0,2,2,1,3,3, 0,3,2,2,3,1, 0,1,2,2,3,3, 0,2,2,3,3,1, 0,3,2,1,3,2) * id;
+    o[0][2] = cof(m, 0,1,1,2,3,3, 0,2,1,3,3,1, 0,3,1,1,3,2, 0,1,1,3,3,2, 0,2,1,1,3,3, 0,3,1,2,3,1) * id;
+    o[0][3] = cof(m, 0,1,1,3,2,2, 0,2,1,1,2,3, 0,3,1,2,2,1, 0,1,1,2,2,3, 0,2,1,3,2,1, 0,3,1,1,2,2) * id;
+    o[1][0] = cof(m, 1,0,2,3,3,2, 1,2,2,0,3,3, 1,3,2,2,3,0, 1,0,2,2,3,3, 1,2,2,3,3,0, 1,3,2,0,3,2) * id;
+    o[1][1] = cof(m, 0,0,2,2,3,3, 0,2,2,3,3,0, 0,3,2,0,3,2, 0,0,2,3,3,2, 0,2,2,0,3,3, 0,3,2,2,3,0) * id;
+    o[1][2] = cof(m, 0,0,1,3,3,2, 0,2,1,0,3,3, 0,3,1,2,3,0, 0,0,1,2,3,3, 0,2,1,3,3,0, 0,3,1,0,3,2) * id;
+    o[1][3] = cof(m, 0,0,1,2,2,3, 0,2,1,3,2,0, 0,3,1,0,2,2, 0,0,1,3,2,2, 0,2,1,0,2,3, 0,3,1,2,2,0) * id;
+    o[2][0] = cof(m, 1,0,2,1,3,3, 1,1,2,3,3,0, 1,3,2,0,3,1, 1,0,2,3,3,1, 1,1,2,0,3,3, 1,3,2,1,3,0) * id;
+    o[2][1] = cof(m, 0,0,2,3,3,1, 0,1,2,0,3,3, 0,3,2,1,3,0, 0,0,2,1,3,3, 0,1,2,3,3,0, 0,3,2,0,3,1) * id;
+    o[2][2] = cof(m, 0,0,1,1,3,3, 0,1,1,3,3,0, 0,3,1,0,3,1, 0,0,1,3,3,1, 0,1,1,0,3,3, 0,3,1,1,3,0) * id;
+    o[2][3] = cof(m, 0,0,1,3,2,1, 0,1,1,0,2,3, 0,3,1,1,2,0, 0,0,1,1,2,3, 0,1,1,3,2,0, 0,3,1,0,2,1) * id;
+    o[3][0] = cof(m, 1,0,2,2,3,1, 1,1,2,0,3,2, 1,2,2,1,3,0, 1,0,2,1,3,2, 1,1,2,2,3,0, 1,2,2,0,3,1) * id;
+    o[3][1] = cof(m, 0,0,2,1,3,2, 0,1,2,2,3,0, 0,2,2,0,3,1, 0,0,2,2,3,1, 0,1,2,0,3,2, 0,2,2,1,3,0) * id;
+    o[3][2] = cof(m, 0,0,1,2,3,1, 0,1,1,0,3,2, 0,2,1,1,3,0, 0,0,1,1,3,2, 0,1,1,2,3,0, 0,2,1,0,3,1) * id;
+    o[3][3] = cof(m, 0,0,1,1,2,2, 0,1,1,2,2,0, 0,2,1,0,2,1, 0,0,1,2,2,1, 0,1,1,0,2,2, 0,2,1,1,2,0) * id;
+}
+// transform.rs:16-107
+void make_matrix(const rs_transform& t, M4 m) {
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) m[i][j] = (i == j) ? 1.0 : 0.0;
+    switch (t.kind) {
+    case RS_TF_TRANSLATE: m[0][3] = t.v[0]; m[1][3] = t.v[1]; m[2][3] = t.v[2]; break;
+    case RS_TF_ROTATE_X: { const double s = std::sin(t.v[0]), c = std::cos(t.v[0]);
+        m[1][1] = c; m[1][2] = s; m[2][1] = -s; m[2][2] = c; break; }
+    case RS_TF_ROTATE_Y: { const double s = std::sin(t.v[0]), c = std::cos(t.v[0]);
+        m[0][0] = c; m[0][2] = s; m[2][0] = -s; m[2][2] = c; break; }
+    case RS_TF_ROTATE_Z: { const double s = std::sin(t.v[0]), c = std::cos(t.v[0]);
+        m[0][0] = c; m[0][1] = s; m[1][0] = -s; m[1][1] = c; break; }
+    case RS_TF_SCALE: m[0][0] = t.v[0]; m[1][1] = t.v[1]; m[2][2] = t.v[2]; m[3][3] = 1.0; break;
+    default: throw Error(RS_E_INVALID, "unknown transform kind");
+    }
+}
+void apply34(const M4 m, const double p[3], double w, double out[3]) {
+    double r[3];
+    for (int i = 0; i < 3; ++i) r[i] = m[i][0] * p[0] + m[i][1] * p[1] + m[i][2] * p[2] + m[i][3] * w;
+    out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
+}
+
+}  // namespace
+
+struct rs_scene {
+    int device = 0;
+    std::vector<rs_material_desc> mdesc;
+    std::vector<HObj> objs;
+    std::vector<uint32_t> world, lights;
+    float bg_lo[3] = {0.3f, 0.4f, 0.5f}, bg_hi[3] = {0.7f, 0.89f, 1.0f};
+    bool committed = false;
+    bool spheres_only = false;
+    bool ref_order = false;                 // BVH::hit recursion order needed (non-monotone objects)
+    DScene ds{};
+    std::vector<void*> dev;                 // scene allocations
+    // render workspace (grown on demand, freed with the scene)
+    double* d_rad = nullptr; size_t rad_cap = 0;
+    double* d_acc = nullptr; size_t acc_cap = 0;
+    unsigned long long* d_cnt = nullptr;
+    uint8_t* d_mask = nullptr; size_t mask_cap = 0;
+    float* d_out = nullptr; size_t out_cap = 0;
+    uint64_t max_items_per_batch = 32ull << 20;
+    int tree_depth = 0;
+    double time0 = 0.0, time1 = 0.0;        // World::new time_limit (world.rs:40-53)
+    std::vector<Box3> boxes;                // per-handle reference bbox (time range [0, 0])
+
+    ~rs_scene() { release(); }
+    void release() {
+        for (void* p : dev) (void)hipFree(p);
+        dev.clear();
+        if (d_rad) (void)hipFree(d_rad);
+        if (d_acc) (void)hipFree(d_acc);
+        if (d_cnt) (void)hipFree(d_cnt);
+        if (d_mask) (void)hipFree(d_mask);
+        if (d_out) (void)hipFree(d_out);
+        d_rad = d_acc = nullptr; d_cnt = nullptr; d_mask = nullptr; d_out = nullptr;
+        rad_cap = acc_cap = mask_cap = out_cap = 0;
+    }
+
+    uint32_t add(HObj o) {
+        if (committed) throw Error(RS_E_STATE, "scene already committed");
+        objs.push_back(std::move(o));
+        return (uint32_t)(objs.size() - 1);
+    }
+    void check_mat(int32_t m) const {
+        if (m != RS_NO_MATERIAL && (m < 0 || (size_t)m >= mdesc.size())) throw Error(RS_E_INVALID, "unknown material id");
+    }
+    void check_handle(uint32_t h) const {
+        if (h >= objs.size()) throw Error(RS_E_INVALID, "unknown object handle");
+    }
+
+    // reference bbox of each handle over World::new's time range [time0, time1]
+    Box3 bbox(uint32_t h) { return bbox_t(h, time0, time1); }
+    Box3 bbox_t(uint32_t h, double time0, double time1) {
+        const HObj& o = objs[h];
+        Box3 r;
+        switch (o.kind) {
+        case PK_SPHERE: {
+            const double* c = o.p; const double rad = o.p[3]; const double* v = o.p + 5;
+            Box3 s, e;
+            if (v[0] == 0.0 && v[1] == 0.0 && v[2] == 0.0) {
+                for (int i = 0; i < 3; ++i) { s.lo[i] = c[i] - rad; s.hi[i] = c[i] + rad; }
+                return s;
+            }
+            for (int i = 0; i < 3; ++i) {
+                double c0 = c[i] + v[i] * time0, c1 = c[i] + v[i] * time1;
+                s.lo[i] = c0 - rad; s.hi[i] = c0 + rad; e.lo[i] = c1 - rad; e.hi[i] = c1 + rad;
+            }
+            return box_union(s, e);
+        }
+        case PK_RECT: {
+            r.lo[o.ax[0]] = o.p[1]; r.lo[o.ax[1]] = o.p[3]; r.lo[o.ax[2]] = o.p[0] - 0.0001;
+            r.hi[o.ax[0]] = o.p[2]; r.hi[o.ax[1]] = o.p[4]; r.hi[o.ax[2]] = o.p[0] + 0.0001;
+            return r;
+        }
+        case PK_BOX: {
+            const double* mn = o.p; const double* mx = o.p + 3;
+            // the six faces in box.rs order; union in list order (list.rs:68-81)
+            struct F { int ax0, ax1, ax2; double k, a0, a1, b0, b1; } f[6] = {
+                {0, 1, 2, mn[2], mn[0], mx[0], mn[1], mx[1]}, {0, 1, 2, mx[2], mn[0], mx[0], mn[1], mx[1]},
+                {1, 2, 0, mn[0], mn[1], mx[1], mn[2], mx[2]}, {1, 2, 0, mx[0], mn[1], mx[1], mn[2], mx[2]},
+                {0, 2, 1, mn[1], mn[0], mx[0], mn[2], mx[2]}, {0, 2, 1, mx[1], mn[0], mx[0], mn[2], mx[2]}};
+            for (int i = 0; i < 6; ++i) {
+                Box3 fb;
+                fb.lo[f[i].ax0] = f[i].a0; fb.lo[f[i].ax1] = f[i].b0; fb.lo[f[i].ax2] = f[i].k - 0.0001;
+                fb.hi[f[i].ax0] = f[i].a1; fb.hi[f[i].ax1] = f[i].b1; fb.hi[f[i].ax2] = f[i].k + 0.0001;
+                r = i == 0 ? fb : box_union(r, fb);
+            }
+            return r;
+        }
+        case PK_QUADRIC:
+            for (int i = 0; i < 3; ++i) { r.lo[i] = -100.0; r.hi[i] = 100.0; }
+            return r;
+        case PK_TRIANGLE: {
+            for (int i = 0; i < 3; ++i) {
+                r.lo[i] = std::fmin(std::fmin(o.p[i], o.p[3 + i]), o.p[6 + i]);
+                r.hi[i] = std::fmax(std::fmax(o.p[i], o.p[3 + i]), o.p[6 + i]);
+            }
+            return r;
+        }
+        case PK_AND: {
+            Box3 b1 = bbox_t((uint32_t)o.a, time0, time1), b2 = bbox_t((uint32_t)o.b, time0, time1);
+            r.lo[0] = std::fmax(b1.lo[0], b2.lo[0]);
+            r.lo[1] = std::fmax(b1.lo[1], b2.lo[1]);
+            r.lo[2] = std::fmax(b1.lo[1], b2.lo[2]);  // intersection.rs:110 uses b1.min.y for z
+            for (int i = 0; i < 3; ++i) r.hi[i] = std::fmin(b1.hi[i], b2.hi[i]);
+            return r;
+        }
+        case PK_SUB: return bbox_t((uint32_t)o.a, time0, time1);
+        case PK_XFORM: {
+            Box3 b = bbox_t((uint32_t)o.a, time0, time1);
+            std::vector<std::vector<double>> fwd;
+            r = box_empty();
+            for (int i = 0; i < 2; ++i) for (int j = 0; j < 2; ++j) for (int k = 0; k < 2; ++k) {
+                double p[3] = {std::fma((double)i, b.hi[0], (double)(1 - i) * b.lo[0]),
+                               std::fma((double)j, b.hi[1], (double)(1 - j) * b.lo[1]),
+                               std::fma((double)k, b.hi[2], (double)(1 - k) * b.lo[2])};
+                for (const rs_transform& t : o.tfs) {
+                    M4 m;
+                    make_matrix(t, m);
+                    apply34(m, p, 1.0, p);
+                }
+                for (int c = 0; c < 3; ++c) { r.lo[c] = std::fmin(r.lo[c], p[c]); r.hi[c] = std::fmax(r.hi[c], p[c]); }
+            }
+            return r;
+        }
+        }
+        throw Error(RS_E_INVALID, "unknown object kind");
+    }
+
+    // true when hit() over [tmin, e) is hit() over [tmin, inf) filtered by t1 < e: then the
+    // closest hit does not depend on the order objects are tested in (up to exact ties)
+    bool monotone(uint32_t h) const {
+        const HObj& o = objs[h];
+        if (o.kind == PK_SPHERE || o.kind == PK_RECT || o.kind == PK_TRIANGLE) return true;
+        if (o.kind == PK_XFORM) return monotone((uint32_t)o.a);
+        return false;  // Box (outside/t2 depend on the far face), Quadric (a < 0 root order), CSG
+    }
+
+    int nest_depth(uint32_t h) const {
+        const HObj& o = objs[h];
+        if (o.kind == PK_AND || o.kind == PK_SUB)
+            return 1 + std::max(nest_depth((uint32_t)o.a), nest_depth((uint32_t)o.b));
+        if (o.kind == PK_XFORM) return 1 + nest_depth((uint32_t)o.a);
+        return 0;
+    }
+};
+
+namespace {
+
+// ---------------------------------------------------------------- BVH (binned SAH) ----
+struct BuildItem { Box3 box; double c[3]; int32_t prim; };
+
+struct Builder {
+    std::vector<DNode> nodes;
+    int max_depth = 0;
+    static double area(const Box3& b) {
+        double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+        if (!std::isfinite(dx) || !std::isfinite(dy) || !std::isfinite(dz)) return 1e300;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+    // returns the child code of the subtree over items[b, e)
+    int32_t build(std::vector<BuildItem>& it, size_t b, size_t e, int depth, Box3& out_box) {
+        if (e - b == 1) { out_box = it[b].box; return ~it[b].prim; }
+        max_depth = std::max(max_depth, depth + 1);
+        Box3 cb = box_empty();
+        for (size_t i = b; i < e; ++i)
+            for (int k = 0; k < 3; ++k) { cb.lo[k] = std::fmin(cb.lo[k], it[i].c[k]); cb.hi[k] = std::fmax(cb.hi[k], it[i].c[k]); }
+        size_t mid = b + (e - b) / 2;
+        int axis = 0;
+        double ext = -1;
+        for (int k = 0; k < 3; ++k) if (cb.hi[k] - cb.lo[k] > ext) { ext = cb.hi[k] - cb.lo[k]; axis = k; }
+        bool done = false;
+        if (depth < 20 && e - b > 2 && ext > 0) {
+            // SAH over a full sweep of the centroid-sorted range on each axis
+            double best_cost = INFINITY; int best_axis = -1; size_t best_split = 0;
+            std::vector<double> right_area(e - b);
+            for (int k = 0; k < 3; ++k) {
+                if (!(cb.hi[k] - cb.lo[k] > 0)) continue;
+                std::stable_sort(it.begin() + b, it.begin() + e, [k](const BuildItem& x, const BuildItem& y) { return x.c[k] < y.c[k]; });
+                Box3 acc = box_empty();
+                for (size_t i = e; i-- > b + 1;) { acc = box_union(acc, it[i].box); right_area[i - b] = area(acc); }
+                acc = box_empty();
+                for (size_t i = b; i + 1 < e; ++i) {
+                    acc = box_union(acc, it[i].box);
+                    double cost = area(acc) * (double)(i + 1 - b) + right_area[i + 1 - b] * (double)(e - i - 1);
+                    if (cost < best_cost) { best_cost = cost; best_axis = k; best_split = i + 1; }
+                }
+            }
+            if (best_axis >= 0) {
+                std::stable_sort(it.begin() + b, it.begin() + e,
+                                 [best_axis](const BuildItem& x, const BuildItem& y) { return x.c[best_axis] < y.c[best_axis]; });
+                mid = best_split;
+                done = true;
+            }
+        }
+        if (!done) {
+            std::stable_sort(it.begin() + b, it.begin() + e, [axis](const BuildItem& x, const BuildItem& y) { return x.c[axis] < y.c[axis]; });
+            mid = b + (e - b) / 2;
+        }
+        const int32_t idx = (int32_t)nodes.size();
+        nodes.emplace_back();
+        Box3 lb, rb;
+        const int32_t l = build(it, b, mid, depth + 1, lb);
+        const int32_t r = build(it, mid, e, depth + 1, rb);
+        DNode& n = nodes[idx];
+        std::memset(&n, 0, sizeof(n));
+        for (int k = 0; k < 3; ++k) { n.lo[0][k] = lb.lo[k]; n.hi[0][k] = lb.hi[k]; n.lo[1][k] = rb.lo[k]; n.hi[1][k] = rb.hi[k]; }
+        n.child[0] = l; n.child[1] = r;
+        out_box = box_union(lb, rb);
+        return idx;
+    }
+};
+
+// BVH::new_internal (bvh.rs:58-113) with find_best_axis (bvh.rs:116-169) instead of the random
+// axis and one object per leaf: the tree the CPU oracle builds, so reference-order traversal
+// visits objects in the same sequence as the oracle's recursion.
+struct RefItem { Box3 box; double key_lo[3]; int32_t prim; };
+int32_t build_ref(std::vector<DNode>& nodes, std::vector<RefItem>& it, size_t b, size_t e, int depth, int& max_depth,
+                  Box3& out) {
+    if (e - b == 1) { out = it[b].box; return ~it[b].prim; }
+    max_depth = std::max(max_depth, depth + 1);
+    Box3 u = it[b].box;
+    for (size_t i = b + 1; i < e; ++i) u = box_union(u, it[i].box);
+    const double sx = u.hi[0] - u.lo[0], sy = u.hi[1] - u.lo[1], sz = u.hi[2] - u.lo[2];
+    int axis = 0;
+    if (sx > sy && sx > sz) axis = 0;
+    else if (sy > sx && sy > sz) axis = 1;
+    else if (sz > sx && sz > sy) axis = 2;
+    std::stable_sort(it.begin() + b, it.begin() + e, [axis](const RefItem& p, const RefItem& q) { return p.key_lo[axis] < q.key_lo[axis]; });
+    const size_t mid = b + (e - b) / 2;
+    const int32_t idx = (int32_t)nodes.size();
+    nodes.emplace_back();
+    Box3 lb, rb;
+    const int32_t l = build_ref(nodes, it, b, mid, depth + 1, max_depth, lb);
+    const int32_t r = build_ref(nodes, it, mid, e, depth + 1, max_depth, rb);
+    DNode& n = nodes[idx];
+    std::memset(&n, 0, sizeof(n));
+    for (int k = 0; k < 3; ++k) { n.lo[0][k] = lb.lo[k]; n.hi[0][k] = lb.hi[k]; n.lo[1][k] = rb.lo[k]; n.hi[1][k] = rb.hi[k]; }
+    n.child[0] = l; n.child[1] = r;
+    out = box_union(lb, rb);
+    return idx;
+}
+
+template <typename T>
+T* upload(rs_scene* s, const std::vector<T>& v) {
+    if (v.empty()) return nullptr;
+    void* p = nullptr;
+    HIP_OK(hipMalloc(&p, v.size() * sizeof(T)));
+    s->dev.push_back(p);
+    HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return (T*)p;
+}
+
+void commit(rs_scene* s) {
+    if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+    HIP_OK(hipGetDevice(&s->device));
+    for (uint32_t h : s->world) if (s->nest_depth(h) > RS_MAX_NEST) throw Error(RS_E_UNSUPPORTED, "object nesting deeper than the GPU path supports");
+    for (uint32_t h : s->lights) if (s->nest_depth(h) > RS_MAX_NEST) throw Error(RS_E_UNSUPPORTED, "light nesting deeper than the GPU path supports");
+
+    // materials (+ the world default material, world.rs:51)
+    std::vector<DMaterial> mats;
+    for (const rs_material_desc& d : s->mdesc) {
+        DMaterial m;
+        std::memset(&m, 0, sizeof(m));
+        m.kind = d.kind; m.tex_kind = d.texture.kind; m.glass = d.glass;
+        m.mix_a = d.mix_a; m.mix_b = d.mix_b;
+        for (int i = 0; i < 4; ++i) { m.even[i] = d.texture.even[i]; m.odd[i] = d.texture.odd[i]; }
+        m.tex_scale = d.texture.scale;
+        m.enter_refractive = 1.0 / d.refractive;   // dielectric.rs:38-46
+        m.outer_refractive = d.refractive;
+        m.exponent = d.exponent; m.multiplier = d.multiplier; m.mix_p = d.mix_p;
+        // settings(): MixedMaterial forwards material_1's (mixed_material.rs:56-58)
+        const rs_material_desc* e = &d;
+        for (int k = 0; k < 64 && e->kind == RS_MAT_MIXED; ++k) e = &s->mdesc[e->mix_a];
+        m.phong_factor = e->phong_factor; m.phong_exponent = e->phong_exponent;
+        mats.push_back(m);
+    }
+    DMaterial dm;
+    std::memset(&dm, 0, sizeof(dm));
+    dm.kind = RS_MAT_LAMBERTIAN; dm.tex_kind = RS_TEX_SOLID;
+    for (int i = 0; i < 4; ++i) dm.even[i] = 1.0f;
+    dm.enter_refractive = dm.outer_refractive = 1.0; dm.multiplier = 1.0; dm.phong_exponent = 1;
+    const int32_t default_mat = (int32_t)mats.size();
+    mats.push_back(dm);
+
+    // lights are needed when any pdf material can be hit (list.rs:51 would panic on % 0)
+    bool needs_lights = false;
+    for (const rs_material_desc& d : s->mdesc)
+        if (d.kind == RS_MAT_LAMBERTIAN || d.kind == RS_MAT_DIFFUSE_METAL || d.kind == RS_MAT_MIXED) needs_lights = true;
+    for (uint32_t h : s->world) {
+        const HObj& o = s->objs[h];
+        if (o.mat == RS_NO_MATERIAL && o.kind <= PK_TRIANGLE) needs_lights = true;
+    }
+    if (needs_lights && s->lights.empty())
+        throw Error(RS_E_NO_LIGHTS, "scene has pdf materials but an empty lights list (reference: % 0 panic, list.rs:51)");
+
+    // flatten every handle
+    std::vector<DPrim> prims(s->objs.size());
+    std::vector<DSphere> spheres; std::vector<DRect> rects; std::vector<DBox> boxes; std::vector<DQuadric> quads;
+    std::vector<DTri> tris; std::vector<DCsg> csgs; std::vector<DXform> xforms; std::vector<DMat34> tf_f, tf_i;
+    for (size_t h = 0; h < s->objs.size(); ++h) {
+        const HObj& o = s->objs[h];
+        DPrim& P = prims[h];
+        P.kind = o.kind; P.mat = o.mat; P.aux = 0;
+        switch (o.kind) {
+        case PK_SPHERE: {
+            DSphere x; for (int i = 0; i < 3; ++i) { x.c[i] = o.p[i]; x.v[i] = o.p[5 + i]; }
+            x.r = o.p[3]; x.r2 = o.p[4];
+            P.idx = (int32_t)spheres.size(); spheres.push_back(x); break;
+        }
+        case PK_RECT: {
+            DRect x; x.ax0 = o.ax[0]; x.ax1 = o.ax[1]; x.ax2 = o.ax[2]; x.pad = 0;
+            x.k = o.p[0]; x.a0 = o.p[1]; x.a1 = o.p[2]; x.b0 = o.p[3]; x.b1 = o.p[4];
+            P.idx = (int32_t)rects.size(); rects.push_back(x); break;
+        }
+        case PK_BOX: {
+            DBox x; for (int i = 0; i < 3; ++i) { x.mn[i] = o.p[i]; x.mx[i] = o.p[3 + i]; }
+            P.idx = (int32_t)boxes.size(); boxes.push_back(x); break;
+        }
+        case PK_QUADRIC: {
+            DQuadric x; for (int i = 0; i < 10; ++i) x.q[i] = o.p[i];
+            P.idx = (int32_t)quads.size(); quads.push_back(x); break;
+        }
+        case PK_TRIANGLE: {
+            DTri x;
+            const double* p0 = o.p; const double* p1 = o.p + 3; const double* p2 = o.p + 6;
+            for (int i = 0; i < 3; ++i) x.p0[i] = p0[i];
+            x.a = p0[0] - p1[0]; x.b = p0[1] - p1[1]; x.c = p0[2] - p1[2];   // triangle_mesh.rs:42-58
+            x.d = p0[0] - p2[0]; x.e = p0[1] - p2[1]; x.f = p0[2] - p2[2];
+            for (int i = 0; i < 3; ++i) { x.n0[i] = o.p[9 + i]; x.n1[i] = o.p[12 + i]; x.n2[i] = o.p[15 + i]; }
+            P.idx = (int32_t)tris.size(); tris.push_back(x); break;
+        }
+        case PK_AND: case PK_SUB: {
+            DCsg x; x.a = o.a; x.b = o.b;
+            P.idx = (int32_t)csgs.size(); csgs.push_back(x); break;
+        }
+        case PK_XFORM: {
+            DXform x; x.child = o.a; x.first = (int32_t)tf_f.size();
+            for (const rs_transform& t : o.tfs) {
+                M4 m, mi;
+                make_matrix(t, m);
+                inv4(m, mi);
+                DMat34 a, b;
+                for (int i = 0; i < 3; ++i) for (int j = 0; j < 4; ++j) { a.m[i][j] = m[i][j]; b.m[i][j] = mi[i][j]; }
+                tf_f.push_back(a); tf_i.push_back(b);
+            }
+            P.aux = (int32_t)o.tfs.size();
+            P.idx = (int32_t)xforms.size(); xforms.push_back(x); break;
+        }
+        default: throw Error(RS_E_INVALID, "unknown object kind");
+        }
+    }
+
+    // BVH over the world list (duplicates in the list are kept as separate leaves, like the reference)
+    std::vector<BuildItem> items;
+    s->spheres_only = true;
+    for (uint32_t h : s->world) {
+        BuildItem bi;
+        bi.box = s->bbox(h);
+        for (int k = 0; k < 3; ++k) {
+            double lo = bi.box.lo[k], hi = bi.box.hi[k];
+            bi.c[k] = (std::isfinite(lo) && std::isfinite(hi)) ? 0.5 * (lo + hi) : 0.0;
+        }
+        bi.prim = (int32_t)h;
+        items.push_back(bi);
+        if (s->objs[h].kind != PK_SPHERE) s->spheres_only = false;
+    }
+    for (uint32_t h : s->lights) if (s->objs[h].kind != PK_SPHERE) s->spheres_only = false;
+    bool all_monotone = true;
+    for (uint32_t h : s->world) all_monotone = all_monotone && s->monotone(h);
+    s->ref_order = !all_monotone;
+    Builder B;
+    int32_t root = -1;
+    if (!items.empty()) {
+        Box3 rb;
+        int32_t code;
+        if (s->ref_order) {
+            std::vector<RefItem> ri;
+            for (uint32_t h : s->world) {
+                RefItem x;
+                x.box = s->bbox(h);
+                const Box3 k = s->bbox_t(h, 0.0, 0.0);  // cmp_geometry_by sorts on bbox(0..0).min (bvh.rs:30-43)
+                for (int a = 0; a < 3; ++a) x.key_lo[a] = k.lo[a];
+                x.prim = (int32_t)h;
+                ri.push_back(x);
+            }
+            code = build_ref(B.nodes, ri, 0, ri.size(), 0, B.max_depth, rb);
+        } else {
+            code = B.build(items, 0, items.size(), 0, rb);
+        }
+        if (code < 0) {  // a single object: wrap it in one node (second slot empty)
+            DNode n;
+            std::memset(&n, 0, sizeof(n));
+            for (int k = 0; k < 3; ++k) { n.lo[0][k] = rb.lo[k]; n.hi[0][k] = rb.hi[k]; n.lo[1][k] = INFINITY; n.hi[1][k] = -INFINITY; }
+            n.child[0] = code; n.child[1] = INT32_MIN;
+            B.nodes.push_back(n);
+            root = 0;
+            B.max_depth = 1;
+        } else {
+            root = code;
+        }
+    }
+    if (B.max_depth > kStackMax) throw Error(RS_E_UNSUPPORTED, "BVH deeper than the traversal stack");
+    s->tree_depth = B.max_depth;
+
+    std::vector<int32_t> lights(s->lights.begin(), s->lights.end());
+    DScene& d = s->ds;
+    std::memset(&d, 0, sizeof(d));
+    d.nodes = upload(s, B.nodes);
+    d.prims = upload(s, prims);
+    d.spheres = upload(s, spheres);
+    d.rects = upload(s, rects);
+    d.boxes = upload(s, boxes);
+    d.quadrics = upload(s, quads);
+    d.tris = upload(s, tris);
+    d.csgs = upload(s, csgs);
+    d.xforms = upload(s, xforms);
+    d.tf_fwd = upload(s, tf_f);
+    d.tf_inv = upload(s, tf_i);
+    d.mats = upload(s, mats);
+    d.lights = upload(s, lights);
+    d.n_lights = (int32_t)lights.size();
+    d.root = root;
+    d.default_mat = default_mat;
+    d.ref_order = s->ref_order ? 1 : 0;
+    for (int i = 0; i < 3; ++i) { d.bg_lo[i] = s->bg_lo[i]; d.bg_hi[i] = s->bg_hi[i]; }
+    d.bg_lo[3] = d.bg_hi[3] = 1.0f;
+    HIP_OK(hipMalloc((void**)&s->d_cnt, 512 * sizeof(unsigned long long)));
+    s->committed = true;
+}
+
+// camera.rs:37-73 with CameraBuilder's aspect = width/height (camera.rs:384-397)
+DCamera make_camera(const rs_camera_desc& c) {
+    auto sub = [](const double* a, const double* b, double* o) { for (int i = 0; i < 3; ++i) o[i] = a[i] - b[i]; };
+    auto len2 = [](const double* a) { return std::fma(a[2], a[2], std::fma(a[0], a[0], a[1] * a[1])); };
+    auto unit = [&](const double* a, double* o) { double inv = 1.0 / std::sqrt(len2(a)); for (int i = 0; i < 3; ++i) o[i] = a[i] * inv; };
+    auto cross = [](const double* a, const double* b, double* o) {
+        double r[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+        o[0] = r[0]; o[1] = r[1]; o[2] = r[2];
+    };
+    const double aspect = (double)c.width / (double)c.height;
+    const double theta = c.fov * (3.14159265358979323846 / 180.0);
+    const double h = std::tan(theta / 2.0);
+    const double vh = 2.0 * h * c.focus;
+    const double vw = vh * aspect;
+    double w[3], d[3], hu[3], vu[3], t[3];
+    sub(c.look_at, c.look_from, d);
+    unit(d, w);
+    cross(w, c.vup, t); unit(t, hu);
+    cross(hu, w, t); unit(t, vu);
+    DCamera o;
+    for (int i = 0; i < 3; ++i) {
+        o.origin[i] = c.look_from[i];
+        o.hf[i] = hu[i] * vw;
+        o.vf[i] = vu[i] * vh;
+        o.hu[i] = hu[i];
+        o.vu[i] = vu[i];
+    }
+    for (int i = 0; i < 3; ++i) {  // look_from - U/2 - V/2 + focus*w  (Div<f64> = * (1/2))
+        double half = 1.0 / 2.0;
+        o.lb[i] = c.look_from[i] - o.hf[i] * half - o.vf[i] * half + w[i] * c.focus;
+    }
+    o.aperture = c.aperture;
+    o.shutter = c.shutter;
+    return o;
+}
+
+uint64_t splitmix64_h(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+template <typename T>
+void ensure(T*& p, size_t& cap, size_t n) {
+    if (n <= cap) return;
+    if (p) HIP_OK(hipFree(p));
+    p = nullptr;
+    HIP_OK(hipMalloc((void**)&p, n * sizeof(T)));
+    cap = n;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        HIP_OK(hipGetDevice(&prev));
+        if (prev != dev) HIP_OK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* d_mask,
+                   float* d_out, hipStream_t stream, rs_render_stats* stats) {
+    if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
+    if (!cam || !st || !d_out) throw Error(RS_E_INVALID, "null argument");
+    if (cam->width == 0 || cam->height == 0) throw Error(RS_E_INVALID, "empty image");
+    if (st->mode == RS_MODE_WAVEFRONT) throw Error(RS_E_UNSUPPORTED, "wavefront mode not built yet");
+    const uint32_t W = cam->width, H = cam->height;
+    const uint32_t rb = st->row_begin;
+    const uint32_t re = st->row_end ? std::min(st->row_end, H) : H;
+    const uint32_t rstep = st->row_step ? st->row_step : 1;
+    if (rb >= re) { if (stats) *stats = rs_render_stats{0, 0, 0.0}; return; }
+    const uint32_t n_rows = (re - rb + rstep - 1) / rstep;
+    const uint64_t n_pix64 = (uint64_t)n_rows * W;
+    if (n_pix64 > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "frame too large");
+    const uint32_t n_pix = (uint32_t)n_pix64;
+    const uint32_t sq = (uint32_t)std::floor(std::sqrt((double)st->samples));  // painter.rs:110-118
+    const uint32_t N = sq * sq;
+
+    DCamera dc = make_camera(*cam);
+    PathParams pp;
+    pp.n_pix_local = n_pix; pp.width = W; pp.height = H; pp.row_begin = rb; pp.row_step = rstep;
+    pp.sqrt_spp = sq; pp.depth = st->depth;
+    pp.key_base = splitmix64_h(splitmix64_h(st->seed) ^ (uint64_t)st->pass);
+    pp.mask = d_mask;
+
+    uint32_t spb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(N, s->max_items_per_batch / n_pix));
+    if (N == 0) spb = 0;
+    ensure(s->d_acc, s->acc_cap, (size_t)3 * n_pix);
+    if (spb) ensure(s->d_rad, s->rad_cap, (size_t)3 * n_pix * spb);
+
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    auto t0 = std::chrono::steady_clock::now();
+    HIP_OK(hipEventRecord(e0, stream));
+    HIP_OK(hipMemsetAsync(s->d_cnt, 0, 512 * sizeof(unsigned long long), stream));
+    if (N == 0) HIP_OK(hipMemsetAsync(s->d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
+    for (uint32_t s0 = 0; s0 < N; s0 += spb) {
+        const uint32_t nb = std::min(spb, N - s0);
+        pp.s0 = s0;
+        pp.n_items = (uint64_t)n_pix * nb;
+        HIP_OK(launch_path_mega(s->ds, dc, pp, s->spheres_only, s->d_rad, s->d_cnt, stream));
+        HIP_OK(launch_accumulate(s->d_rad, s->d_acc, n_pix, nb, s0 == 0, stream));
+    }
+    FinalParams fp;
+    fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rb; fp.row_step = rstep; fp.n_samples = N;
+    fp.gamma = st->gamma; fp.mask = d_mask;
+    HIP_OK(launch_finalize(s->d_acc, d_out, fp, stream));
+    HIP_OK(hipEventRecord(e1, stream));
+    unsigned long long cnt[512];
+    HIP_OK(hipMemcpyAsync(cnt, s->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    auto t1 = std::chrono::steady_clock::now();
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (stats) {
+        uint64_t seg = 0;
+        for (int i = 0; i < 256; ++i) seg += cnt[i];
+        stats->segments = seg;
+        stats->samples = (uint64_t)n_pix * N;  // masked-out pixels included (they trace nothing)
+        stats->ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        (void)ms;
+    }
+}
+
+}  // namespace
+
+namespace {
+int run(const std::function<void()>& f) {
+    try {
+        f();
+        return RS_OK;
+    } catch (const Error& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "out of host memory";
+        return RS_E_NOMEM;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return RS_E_INVALID;
+    }
+}
+rs_scene* S(rs_scene* s) {
+    if (!s) throw Error(RS_E_INVALID, "null scene");
+    return s;
+}
+}  // namespace
+
+extern "C" {
+
+int rs_abi_version(void) { return RS_ABI_VERSION; }
+const char* rs_last_error(void) { return g_last_error.c_str(); }
+int rs_device_count(int* count) {
+    return run([&] { if (!count) throw Error(RS_E_INVALID, "null"); HIP_OK(hipGetDeviceCount(count)); });
+}
+uint64_t rs_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
+    return splitmix64_h(splitmix64_h(splitmix64_h(splitmix64_h(seed) ^ (uint64_t)pass) ^ pixel) ^ (uint64_t)sample);
+}
+
+int rs_scene_create(rs_scene** out) {
+    return run([&] { if (!out) throw Error(RS_E_INVALID, "null"); *out = new rs_scene(); });
+}
+int rs_scene_destroy(rs_scene* s) {
+    return run([&] { delete s; });
+}
+int rs_material(rs_scene* s, const rs_material_desc* d, int32_t* id) {
+    return run([&] {
+        S(s);
+        if (!d || !id) throw Error(RS_E_INVALID, "null argument");
+        if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+        if (d->kind < RS_MAT_LAMBERTIAN || d->kind > RS_MAT_MIXED) throw Error(RS_E_INVALID, "unknown material kind");
+        if (d->texture.kind != RS_TEX_SOLID && d->texture.kind != RS_TEX_CHECKER) throw Error(RS_E_INVALID, "unknown texture kind");
+        if (d->kind == RS_MAT_MIXED) {
+            if (d->mix_a < 0 || (size_t)d->mix_a >= s->mdesc.size() || d->mix_b < 0 || (size_t)d->mix_b >= s->mdesc.size())
+                throw Error(RS_E_INVALID, "mixed material refers to unknown ids");
+        }
+        *id = (int32_t)s->mdesc.size();
+        s->mdesc.push_back(*d);
+    });
+}
+int rs_sphere(rs_scene* s, const double c[3], double r, const double v[3], int32_t mat, uint32_t* out) {
+    return run([&] {
+        S(s)->check_mat(mat);
+        if (!c || !out) throw Error(RS_E_INVALID, "null argument");
+        HObj o; o.kind = PK_SPHERE; o.mat = mat;
+        o.p[0] = c[0]; o.p[1] = c[1]; o.p[2] = c[2]; o.p[3] = r; o.p[4] = r * r;  // sphere.rs:35-43
+        if (v) { o.p[5] = v[0]; o.p[6] = v[1]; o.p[7] = v[2]; }
+        *out = s->add(o);
+    });
+}
+int rs_aarect(rs_scene* s, int32_t plane, double k, double a0, double a1, double b0, double b1, int32_t mat, uint32_t* out) {
+    return run([&] {
+        S(s)->check_mat(mat);
+        if (!out) throw Error(RS_E_INVALID, "null argument");
+        if (!(a0 < a1) || !(b0 < b1)) throw Error(RS_E_INVALID, "AARectMetrics requires a0 < a1 and b0 < b1 (rect.rs:27-28)");
+        HObj o; o.kind = PK_RECT; o.mat = mat;
+        if (plane == RS_PLANE_XY) { o.ax[0] = 0; o.ax[1] = 1; o.ax[2] = 2; }
+        else if (plane == RS_PLANE_XZ) { o.ax[0] = 0; o.ax[1] = 2; o.ax[2] = 1; }
+        else if (plane == RS_PLANE_YZ) { o.ax[0] = 1; o.ax[1] = 2; o.ax[2] = 0; }
+        else throw Error(RS_E_INVALID, "bad plane");
+        o.p[0] = k; o.p[1] = a0; o.p[2] = a1; o.p[3] = b0; o.p[4] = b1;
+        *out = s->add(o);
+    });
+}
+int rs_box(rs_scene* s, const double p0[3], const double p1[3], int32_t mat, uint32_t* out) {
+    return run([&] {
+        S(s)->check_mat(mat);
+        if (!p0 || !p1 || !out) throw Error(RS_E_INVALID, "null argument");
+        HObj o; o.kind = PK_BOX; o.mat = mat;
+        for (int i = 0; i < 3; ++i) { o.p[i] = std::fmin(p0[i], p1[i]); o.p[3 + i] = std::fmax(p0[i], p1[i]); }  // box.rs:40-45
+        for (int i = 0; i < 3; ++i)
+            if (!(o.p[i] < o.p[3 + i])) throw Error(RS_E_INVALID, "degenerate box: face metrics need a0 < a1 (rect.rs:27-28)");
+        *out = s->add(o);
+    });
+}
+int rs_quadric(rs_scene* s, const double q[10], int32_t mat, uint32_t* out) {
+    return run([&] {
+        S(s)->check_mat(mat);
+        if (!q || !out) throw Error(RS_E_INVALID, "null argument");
+        HObj o; o.kind = PK_QUADRIC; o.mat = mat;
+        for (int i = 0; i < 10; ++i) o.p[i] = q[i];
+        *out = s->add(o);
+    });
+}
+int rs_triangles(rs_scene* s, const double* pos, const double* nrm, uint32_t n, int32_t mat, uint32_t* first) {
+    return run([&] {
+        S(s)->check_mat(mat);
+        if (!pos || !first) throw Error(RS_E_INVALID, "null argument");
+        *first = (uint32_t)s->objs.size();
+        for (uint32_t i = 0; i < n; ++i) {
+            HObj o; o.kind = PK_TRIANGLE; o.mat = mat;
+            for (int j = 0; j < 9; ++j) o.p[j] = pos[9 * (size_t)i + j];
+            for (int j = 0; j < 9; ++j) o.p[9 + j] = nrm ? nrm[9 * (size_t)i + j] : 0.0;
+            s->add(o);
+        }
+    });
+}
+int rs_intersection(rs_scene* s, uint32_t a, uint32_t b, int32_t mat, uint32_t* out) {
+    return run([&] {
+        S(s)->check_mat(mat); s->check_handle(a); s->check_handle(b);
+        if (!out) throw Error(RS_E_INVALID, "null argument");
+        HObj o; o.kind = PK_AND; o.mat = mat; o.a = (int32_t)a; o.b = (int32_t)b;
+        *out = s->add(o);
+    });
+}
+int rs_difference(rs_scene* s, uint32_t a, uint32_t b, int32_t mat, uint32_t* out) {
+    return run([&] {
+        S(s)->check_mat(mat); s->check_handle(a); s->check_handle(b);
+        if (!out) throw Error(RS_E_INVALID, "null argument");
+        HObj o; o.kind = PK_SUB; o.mat = mat; o.a = (int32_t)a; o.b = (int32_t)b;
+        *out = s->add(o);
+    });
+}
+int rs_transformed(rs_scene* s, uint32_t obj, const rs_transform* st, uint32_t n, uint32_t* out) {
+    return run([&] {
+        S(s)->check_handle(obj);
+        if (!out || (n && !st)) throw Error(RS_E_INVALID, "null argument");
+        HObj o; o.kind = PK_XFORM; o.a = (int32_t)obj;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (st[i].kind < RS_TF_TRANSLATE || st[i].kind > RS_TF_SCALE) throw Error(RS_E_INVALID, "unknown transform kind");
+            o.tfs.push_back(st[i]);
+        }
+        o.mat = s->objs[obj].mat;  // TfFacade::material is never called upstream; kept for needs_lights
+        *out = s->add(o);
+    });
+}
+int rs_world_add(rs_scene* s, uint32_t h) {
+    return run([&] { S(s)->check_handle(h); if (s->committed) throw Error(RS_E_STATE, "scene already committed"); s->world.push_back(h); });
+}
+int rs_lights_add(rs_scene* s, uint32_t h) {
+    return run([&] { S(s)->check_handle(h); if (s->committed) throw Error(RS_E_STATE, "scene already committed"); s->lights.push_back(h); });
+}
+int rs_set_background(rs_scene* s, const float lo[3], const float hi[3]) {
+    return run([&] {
+        S(s);
+        if (!lo || !hi) throw Error(RS_E_INVALID, "null argument");
+        if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+        for (int i = 0; i < 3; ++i) { s->bg_lo[i] = lo[i]; s->bg_hi[i] = hi[i]; }
+    });
+}
+int rs_set_time_range(rs_scene* s, double t0, double t1) {
+    return run([&] {
+        S(s);
+        if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+        s->time0 = t0; s->time1 = t1;
+    });
+}
+int rs_scene_commit(rs_scene* s) {
+    return run([&] { commit(S(s)); });
+}
+
+int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* d_mask,
+                     float* d_out, void* stream, rs_render_stats* stats) {
+    return run([&] {
+        S(s);
+        DeviceGuard g(s->device);
+        render_device(s, cam, st, d_mask, d_out, (hipStream_t)stream, stats);
+    });
+}
+
+int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin, double tmax, double* out) {
+    return run([&] {
+        S(s);
+        if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
+        if (!rays || !out) throw Error(RS_E_INVALID, "null argument");
+        DeviceGuard g(s->device);
+        double *dr = nullptr, *dout = nullptr;
+        HIP_OK(hipMalloc((void**)&dr, (size_t)n * 7 * sizeof(double) + 8));
+        HIP_OK(hipMalloc((void**)&dout, (size_t)n * 13 * sizeof(double) + 8));
+        HIP_OK(hipMemcpy(dr, rays, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice));
+        HIP_OK(launch_probe_hit(s->ds, dr, n, tmin, tmax, dout, nullptr));
+        HIP_OK(hipMemcpy(out, dout, (size_t)n * 13 * sizeof(double), hipMemcpyDeviceToHost));
+        (void)hipFree(dr);
+        (void)hipFree(dout);
+    });
+}
+
+int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask, float* out,
+              rs_render_stats* stats) {
+    return run([&] {
+        S(s);
+        if (!cam || !out) throw Error(RS_E_INVALID, "null argument");
+        DeviceGuard g(s->device);
+        const size_t npx = (size_t)cam->width * cam->height;
+        ensure(s->d_out, s->out_cap, npx * 4);
+        // rows not rendered keep the caller's values: seed the device frame with them
+        HIP_OK(hipMemcpy(s->d_out, out, npx * 4 * sizeof(float), hipMemcpyHostToDevice));
+        const uint8_t* dm = nullptr;
+        if (mask) {
+            ensure(s->d_mask, s->mask_cap, npx);
+            HIP_OK(hipMemcpy(s->d_mask, mask, npx, hipMemcpyHostToDevice));
+            dm = s->d_mask;
+        }
+        render_device(s, cam, st, dm, s->d_out, nullptr, stats);
+        HIP_OK(hipMemcpy(out, s->d_out, npx * 4 * sizeof(float), hipMemcpyDeviceToHost));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// rs_layout.h — device-resident scene layout (host builds it, kernels read it).
+//
+// Everything is f64, the reference's arithmetic type (src/prelude/vec3.rs:14-19); colours stay
+// f32 like the reference's Color (src/prelude/color.rs:11-16). The scene for every config fits
+// in a few MB, so it is L2/MALL-resident during a frame; per-path state is what streams.
+#pragma once
+#include <stdint.h>
+
+#define RS_MAX_NEST 4   // object nesting levels supported on the GPU (TfFacade / CSG chains)
+
+namespace rs {
+
+enum PrimKind : int32_t {
+    PK_SPHERE = 0,
+    PK_RECT = 1,
+    PK_BOX = 2,
+    PK_QUADRIC = 3,
+    PK_TRIANGLE = 4,
+    PK_AND = 5,     // csg Intersection  (src/hittable/csg/intersection.rs)
+    PK_SUB = 6,     // csg Difference    (src/hittable/csg/difference.rs)
+    PK_XFORM = 7,   // TfFacade          (src/hittable/transform/tf_facade.rs)
+};
+
+// One entry per hittable handle (world objects and nested children alike).
+struct DPrim {
+    int32_t kind;
+    int32_t idx;   // index into the per-kind array
+    int32_t mat;   // material id, -1 = None
+    int32_t aux;   // XFORM: number of transforms; CSG: unused
+};
+
+struct DSphere {   // sphere.rs:16-23
+    double c[3];
+    double r;
+    double r2;     // radius_squared
+    double v[3];   // speed
+};
+
+struct DRect {     // rect.rs:178-212
+    int32_t ax0, ax1, ax2, pad;
+    double k, a0, a1, b0, b1;
+};
+
+struct DBox {      // box.rs:331-336 (faces are derived from min/max in the reference order)
+    double mn[3];
+    double mx[3];
+};
+
+struct DQuadric {  // quadric.rs:20-34, field order qa qb qc qd qe qf qg qh qi qj
+    double q[10];
+};
+
+struct DTri {      // triangle_mesh.rs:14-26
+    double p0[3];
+    double a, b, c, d, e, f;
+    double n0[3], n1[3], n2[3];
+};
+
+struct DCsg {      // Intersection(o1, o2) / Difference(plus, minus): prim indices
+    int32_t a, b;
+};
+
+struct DXform {    // TfFacade: child prim + transforms [first, first+n) of the matrix table
+    int32_t child;
+    int32_t first;
+};
+
+// rows 0..2 of the 4x4 row-major matrix (row 3 is never read by row_mat4_transform's xyz)
+struct DMat34 {
+    double m[3][4];
+};
+
+struct DMaterial { // src/material/*.rs flattened
+    int32_t kind;        // RS_MAT_*
+    int32_t tex_kind;    // RS_TEX_*
+    int32_t glass;
+    int32_t mix_a, mix_b;
+    int32_t phong_exponent;  // effective settings() (MixedMaterial -> material_1's)
+    float even[4];
+    float odd[4];
+    double tex_scale;
+    double enter_refractive, outer_refractive;
+    double exponent;
+    double multiplier;
+    double mix_p;
+    double phong_factor;
+};
+
+// Binary BVH node: both child boxes live in the parent, so one node fetch tests two children.
+// child >= 0: inner node index; child < 0: leaf, prim index = ~child.
+struct alignas(16) DNode {
+    double lo[2][3];
+    double hi[2][3];
+    int32_t child[2];
+    int32_t pad[2];
+};
+
+struct DScene {
+    const DNode* nodes;
+    const DPrim* prims;
+    const DSphere* spheres;
+    const DRect* rects;
+    const DBox* boxes;
+    const DQuadric* quadrics;
+    const DTri* tris;
+    const DCsg* csgs;
+    const DXform* xforms;
+    const DMat34* tf_fwd;
+    const DMat34* tf_inv;
+    const DMaterial* mats;
+    const int32_t* lights;   // prim indices
+    int32_t n_lights;
+    int32_t root;            // root child code (node index, or ~prim if a single object, or INT32_MIN if empty)
+    int32_t default_mat;     // world.rs:51 Lambertian(Color(1,1,1,1))
+    int32_t ref_order;       // 1: traverse in BVH::hit's recursion order (bvh.rs:173-192); 0: near-first
+    float bg_lo[4], bg_hi[4];
+};
+
+struct DCamera {   // camera.rs:18-31
+    double origin[3], lb[3], hf[3], vf[3], hu[3], vu[3];
+    double aperture, shutter;
+};
+
+}  // namespace rs
