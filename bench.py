@@ -1,0 +1,177 @@
+"""bench.py — BASELINE metric: Msamples/s (whole node) + ms/frame on the RTIOW-13.1 scene
+(examples/rtow_13_1.rs: balls_scene seed 7 + light sphere) at 800x500, 64 spp, depth 8.
+
+A step = one frame pass of that workload per GPU (inputs resident in HBM: the scene is committed
+before timing, the frame lands in a device buffer). --split passes (default, weak scaling): rank
+r renders progressive pass r and the passes are combined at frame end (RCCL all_gather);
+--split rows (strong scaling): the frame's rows are interleaved over ranks and gathered.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
+torch.distributed.run with one rank per GPU. Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+STATE_BYTES_PER_SEGMENT = 212  # extend 28+16, shade 76+16+76
+STATE_BYTES_PER_SAMPLE = 124   # generate 76, finalize 16+32
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cam, world, spp, depth, seed, row_step, threads):
+    """The oracle (C++ restatement of Painter::draw, f64, row-interleaved threads) on a bounded row
+    subset of the same frame. kind = 'port'."""
+    from oracle.binding import OracleScene
+    from raysnail_amd import _abi as A
+    st = A.rs_render_settings()
+    st.samples, st.depth, st.gamma, st.seed = spp, depth, 1, seed
+    st.row_begin, st.row_end, st.row_step = 0, 0, row_step
+    sc = OracleScene(world)
+    t0 = time.perf_counter()
+    _, stats = sc.render(cam.desc, st, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": stats.samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"every {row_step}th row of the 800x500x64 frame ({stats.samples} samples, "
+                      f"{stats.segments} segments) in {dt:.1f} s, {threads} threads, oracle/oracle.cpp f64"}
+
+
+def load_pmc(kernel_prefix):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary (tools/collect_pmc.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        k = d.get(kernel_prefix)
+        return None if k is None else float(k["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=800)
+    ap.add_argument("--height", type=int, default=500)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--split", choices=["passes", "rows"], default="passes")
+    ap.add_argument("--mode", type=int, default=0, help="RS_MODE_* (0 auto)")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-row-step", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from raysnail_amd import scenes
+    from raysnail_amd.distributed import render_sharded
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cam, scene_world, _, _ = scenes.rtow_13_1(args.width, args.height)
+    photo = cam.take_photo().samples(args.spp).depth(args.depth).seed(args.seed).mode(args.mode)
+    ds = scene_world.device_scene()  # BVH build + upload: outside the timed region
+    H, W = args.height, args.width
+    frame = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    last = {}
+
+    def render(rb, re, rs, pass_index):
+        st = photo.rows(rb, re, rs).pass_index(pass_index).settings()
+        stats = ds.render_device(cam.desc, st, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        last["stats"] = stats
+        return frame
+
+    def step():
+        return render_sharded(render, rank, world, args.split)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    path_ms = []
+    segs = 0
+    samples = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = last["stats"]
+        path_ms.append(st.path_ms / max(1, st.launches))
+        segs += st.segments
+        samples += st.samples
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([float(samples), float(segs)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    dt = float(t.item())
+    all_samples, all_segs = float(tot[0].item()), float(tot[1].item())
+
+    if rank == 0:
+        n_eff = int(args.spp ** 0.5) ** 2
+        value = all_samples / dt / 1e6
+        # roofline of the dominant kernel (the path-tracing launch), rank 0's launches
+        my_samples_per_launch = samples / max(1, args.steps * max(1, last["stats"].launches))
+        my_segs_per_launch = segs / max(1, args.steps * max(1, last["stats"].launches))
+        alg_bytes = STATE_BYTES_PER_SEGMENT * my_segs_per_launch + STATE_BYTES_PER_SAMPLE * my_samples_per_launch
+        avg_launch_s = sum(path_ms) / len(path_ms) / 1e3
+        achieved = alg_bytes / avg_launch_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc("k_path_mega"),
+                "kernel": "k_path_mega", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                "alg_bytes_per_launch": int(alg_bytes),
+                "segments_per_sample": round(my_segs_per_launch / max(1.0, my_samples_per_launch), 4)}
+        cpu = None
+        if args.cpu_baseline and world == 1:
+            log("timing CPU baseline (oracle restatement) ...")
+            cpu = cpu_baseline(cam, scene_world, args.spp, args.depth, args.seed, args.cpu_row_step,
+                               args.cpu_threads)
+        line = {
+            "metric": "Msamples/s (whole node) + ms/frame, RTIOW-13.1 scene 800x500x64spp",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak" if args.split == "passes" else "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: RTIOW final scene regenerated from seed 7 (restated ChaCha12), per-sample RNG streams",
+            "config": {"workload": f"rtow_13_1 balls_scene(seed 7)+light, {W}x{H}, {n_eff} spp, depth {args.depth}",
+                       "width": W, "height": H, "spp": n_eff, "depth": args.depth, "split": args.split,
+                       "samples_per_frame": W * H * n_eff, "frames_per_step": world if args.split == "passes" else 1},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -151,6 +151,9 @@ typedef struct rs_render_stats {
     uint64_t samples;    /* camera samples traced */
     uint64_t segments;   /* world.hit calls (path segments) */
     double   ms;         /* wall time inside the call (device work + sync) */
+    double   path_ms;    /* device time of the path-tracing launches (HIP events on the call's stream) */
+    uint32_t launches;   /* number of path-tracing launches in the call */
+    uint32_t _pad;
 } rs_render_stats;
 
 typedef struct rs_scene rs_scene;

@@ -71,7 +71,8 @@ class rs_render_settings(C.Structure):
 
 
 class rs_render_stats(C.Structure):
-    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("ms", C.c_double)]
+    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("ms", C.c_double), ("path_ms", C.c_double),
+                ("launches", C.c_uint32), ("_pad", C.c_uint32)]
 
 
 D3 = C.c_double * 3

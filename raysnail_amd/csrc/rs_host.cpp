@@ -18,6 +18,7 @@
 #include <functional>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -154,7 +155,7 @@ struct rs_scene {
     unsigned long long* d_cnt = nullptr;
     uint8_t* d_mask = nullptr; size_t mask_cap = 0;
     float* d_out = nullptr; size_t out_cap = 0;
-    uint64_t max_items_per_batch = 32ull << 20;
+    uint64_t max_items_per_batch = 32ull << 20;  // RS_MAX_BATCH_ITEMS overrides (tests)
     int tree_depth = 0;
     double time0 = 0.0, time1 = 0.0;        // World::new time_limit (world.rs:40-53)
     std::vector<Box3> boxes;                // per-handle reference bbox (time range [0, 0])
@@ -390,7 +391,6 @@ T* upload(rs_scene* s, const std::vector<T>& v) {
 
 void commit(rs_scene* s) {
     if (s->committed) throw Error(RS_E_STATE, "scene already committed");
-    HIP_OK(hipGetDevice(&s->device));
     for (uint32_t h : s->world) if (s->nest_depth(h) > RS_MAX_NEST) throw Error(RS_E_UNSUPPORTED, "object nesting deeper than the GPU path supports");
     for (uint32_t h : s->lights) if (s->nest_depth(h) > RS_MAX_NEST) throw Error(RS_E_UNSUPPORTED, "light nesting deeper than the GPU path supports");
 
@@ -431,6 +431,7 @@ void commit(rs_scene* s) {
     if (needs_lights && s->lights.empty())
         throw Error(RS_E_NO_LIGHTS, "scene has pdf materials but an empty lights list (reference: % 0 panic, list.rs:51)");
 
+    HIP_OK(hipGetDevice(&s->device));
     // flatten every handle
     std::vector<DPrim> prims(s->objs.size());
     std::vector<DSphere> spheres; std::vector<DRect> rects; std::vector<DBox> boxes; std::vector<DQuadric> quads;
@@ -637,7 +638,7 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
     const uint32_t rb = st->row_begin;
     const uint32_t re = st->row_end ? std::min(st->row_end, H) : H;
     const uint32_t rstep = st->row_step ? st->row_step : 1;
-    if (rb >= re) { if (stats) *stats = rs_render_stats{0, 0, 0.0}; return; }
+    if (rb >= re) { if (stats) *stats = rs_render_stats{0, 0, 0.0, 0.0, 0, 0}; return; }
     const uint32_t n_rows = (re - rb + rstep - 1) / rstep;
     const uint64_t n_pix64 = (uint64_t)n_rows * W;
     if (n_pix64 > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "frame too large");
@@ -657,40 +658,45 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
     ensure(s->d_acc, s->acc_cap, (size_t)3 * n_pix);
     if (spb) ensure(s->d_rad, s->rad_cap, (size_t)3 * n_pix * spb);
 
-    hipEvent_t e0, e1;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
+    const uint32_t n_batches = spb ? (N + spb - 1) / spb : 0;
+    std::vector<hipEvent_t> ev(2 * (size_t)n_batches);
+    for (auto& e : ev) HIP_OK(hipEventCreate(&e));
     auto t0 = std::chrono::steady_clock::now();
-    HIP_OK(hipEventRecord(e0, stream));
     HIP_OK(hipMemsetAsync(s->d_cnt, 0, 512 * sizeof(unsigned long long), stream));
     if (N == 0) HIP_OK(hipMemsetAsync(s->d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
-    for (uint32_t s0 = 0; s0 < N; s0 += spb) {
+    uint32_t bi = 0;
+    for (uint32_t s0 = 0; s0 < N; s0 += spb, ++bi) {
         const uint32_t nb = std::min(spb, N - s0);
         pp.s0 = s0;
         pp.n_items = (uint64_t)n_pix * nb;
+        HIP_OK(hipEventRecord(ev[2 * bi], stream));
         HIP_OK(launch_path_mega(s->ds, dc, pp, s->spheres_only, s->d_rad, s->d_cnt, stream));
+        HIP_OK(hipEventRecord(ev[2 * bi + 1], stream));
         HIP_OK(launch_accumulate(s->d_rad, s->d_acc, n_pix, nb, s0 == 0, stream));
     }
     FinalParams fp;
     fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rb; fp.row_step = rstep; fp.n_samples = N;
     fp.gamma = st->gamma; fp.mask = d_mask;
     HIP_OK(launch_finalize(s->d_acc, d_out, fp, stream));
-    HIP_OK(hipEventRecord(e1, stream));
     unsigned long long cnt[512];
     HIP_OK(hipMemcpyAsync(cnt, s->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     auto t1 = std::chrono::steady_clock::now();
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    double path_ms = 0.0;
+    for (uint32_t b = 0; b < n_batches; ++b) {
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, ev[2 * b], ev[2 * b + 1]));
+        path_ms += ms;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
     if (stats) {
+        stats->path_ms = path_ms;
+        stats->launches = n_batches;
         uint64_t seg = 0;
         for (int i = 0; i < 256; ++i) seg += cnt[i];
         stats->segments = seg;
         stats->samples = (uint64_t)n_pix * N;  // masked-out pixels included (they trace nothing)
         stats->ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        (void)ms;
     }
 }
 
@@ -730,7 +736,15 @@ uint64_t rs_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sa
 }
 
 int rs_scene_create(rs_scene** out) {
-    return run([&] { if (!out) throw Error(RS_E_INVALID, "null"); *out = new rs_scene(); });
+    return run([&] {
+        if (!out) throw Error(RS_E_INVALID, "null");
+        rs_scene* s = new rs_scene();
+        if (const char* e = std::getenv("RS_MAX_BATCH_ITEMS")) {
+            const unsigned long long v = std::strtoull(e, nullptr, 10);
+            if (v) s->max_items_per_batch = v;
+        }
+        *out = s;
+    });
 }
 int rs_scene_destroy(rs_scene* s) {
     return run([&] { delete s; });
@@ -865,6 +879,7 @@ int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
                      float* d_out, void* stream, rs_render_stats* stats) {
     return run([&] {
         S(s);
+        if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
         DeviceGuard g(s->device);
         render_device(s, cam, st, d_mask, d_out, (hipStream_t)stream, stats);
     });
@@ -892,6 +907,7 @@ int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* 
     return run([&] {
         S(s);
         if (!cam || !out) throw Error(RS_E_INVALID, "null argument");
+        if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
         DeviceGuard g(s->device);
         const size_t npx = (size_t)cam->width * cam->height;
         ensure(s->d_out, s->out_cap, npx * 4);

@@ -1,0 +1,86 @@
+"""Multi-GPU sharding of the render path: one process per GPU, torch.distributed (RCCL over xGMI
+on MI355X, gloo in the CPU tests).
+
+raysnail itself only splits rows over CPU threads (src/painter.rs:239-299: thread i renders rows
+i, i+T, ... and Painter::append de-interleaves them). The GPU path keeps both of the reference's
+natural shardings, each with a single exchange at frame end:
+
+* ``rows``   — one frame, rows interleaved over ranks exactly like render_rows (row r on rank
+               r % N); ranks pack their rows, all_gather them and de-interleave (= append,
+               painter.rs:220-236). Strong scaling; the assembled frame is bitwise equal to the
+               1-GPU frame because every sample has its own RNG stream.
+* ``passes`` — the CLI's progressive passes (src/bin/raysnail.rs:379-427): rank r renders pass r
+               of the whole frame; the N pass frames are gathered and folded in pass order with
+               combine_pixel (raysnail.rs:176-208). Weak scaling: per-GPU work is one full pass.
+
+The renderer is injected (``render(row_begin, row_end, row_step, pass_index) -> (H, W, 4)``), so
+the same code runs over libraysnail_hip on the GPU and over the CPU oracle in the gloo tests.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+import torch.distributed as dist
+
+
+def row_lattice(rank: int, world: int):
+    """Rows of rank `rank`: rank, rank + world, ... (painter.rs:248)."""
+    return rank, 0, world
+
+
+def rows_of(rank: int, world: int, height: int) -> int:
+    return (height - rank + world - 1) // world if rank < height else 0
+
+
+def gather_rows(frame: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    """frame: (H, W, 4) with this rank's lattice rows rendered. Returns the full frame on every rank."""
+    H = frame.shape[0]
+    if world == 1:
+        return frame
+    per = (H + world - 1) // world
+    mine = frame[rank::world]
+    packed = torch.zeros((per,) + tuple(frame.shape[1:]), dtype=frame.dtype, device=frame.device)
+    packed[: mine.shape[0]] = mine
+    parts = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(parts, packed)
+    out = torch.empty_like(frame)
+    for r in range(world):
+        n = rows_of(r, world, H)
+        out[r::world] = parts[r][:n]
+    return out
+
+
+def combine_pixels(old: torch.Tensor, new: torch.Tensor, p: float) -> torch.Tensor:
+    """raysnail.rs:176-208: keep old where new is [0,0,0,0], else (old*p + new)/(p+1), f32."""
+    empty = (new == 0).all(dim=-1, keepdim=True)
+    pp = torch.tensor(p, dtype=torch.float32, device=new.device)
+    mixed = (old * pp + new) / (pp + 1.0)
+    return torch.where(empty, old, mixed)
+
+
+def gather_passes(frame: torch.Tensor, rank: int, world: int, dst: int = 0):
+    """All ranks' pass frames -> rank `dst` folds them in pass order (starting from the CLI's
+    initial [0,0,0,1] image, raysnail.rs:317-322). Returns the combined frame on dst, else None."""
+    if world == 1:
+        parts = [frame]
+    else:
+        parts = [torch.empty_like(frame) for _ in range(world)]
+        dist.all_gather(parts, frame)
+    if rank != dst:
+        return None
+    acc = torch.zeros_like(frame)
+    acc[..., 3] = 1.0
+    for p, f in enumerate(parts):
+        acc = combine_pixels(acc, f, float(p))
+    return acc
+
+
+def render_sharded(render: Callable[[int, int, int, int], torch.Tensor], rank: int, world: int, split: str):
+    """One frame step of the job. split = 'rows' (strong) or 'passes' (weak)."""
+    if split == "rows":
+        rb, re, rs = row_lattice(rank, world)
+        return gather_rows(render(rb, re, rs, 0), rank, world)
+    if split == "passes":
+        return gather_passes(render(0, 0, 1, rank), rank, world)
+    raise ValueError(split)

@@ -1,0 +1,192 @@
+"""GPU parity: libraysnail_hip (gfx950) against the CPU oracle on the same seeded inputs.
+
+North-star tolerance (BASELINE.json): per-pixel RMSE < 1e-4 against the reference semantics at a
+fixed seed. The GPU path computes in f64 with the reference's operation order, so in practice the
+frames are bit-identical; the tests assert the RMSE bound and, more strictly, >= 99.9 % bitwise
+identical pixels (the remainder would be ocml-vs-glibc ulp differences in sin/cos/pow).
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+
+from raysnail_amd import _abi as A
+from raysnail_amd import scenes
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _oracle(world):
+    from oracle.binding import OracleScene
+    return OracleScene(world)
+
+
+def _cmp(gpu_img, ref_img):
+    g = gpu_img[..., :3].astype(np.float64)
+    r = ref_img[..., :3].astype(np.float64)
+    d = np.abs(g - r)
+    rmse = float(np.sqrt(np.mean(d * d)))
+    exact = float(np.mean(np.all(gpu_img == ref_img, axis=-1)))
+    return rmse, exact, float(d.max())
+
+
+def _load_make_golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg
+
+
+@pytest.mark.parametrize("name", ["rtow", "example_sdl", "quadric_sdl", "cornell", "rtow_depth50"])
+def test_golden_frames(gpu, name):
+    mg = _load_make_golden()
+    build, spp, depth, seed = mg.FRAMES[name]
+    cam, world = build()
+    photo = cam.take_photo().samples(spp).depth(depth).seed(seed)
+    img = photo.shot(None, world)
+    ref = np.load(os.path.join(GOLDEN, "oracle_frames.npz"))[name]
+    rmse, exact, mx = _cmp(img, ref)
+    kat = json.load(open(os.path.join(GOLDEN, "kat.json")))
+    assert photo.last_stats.segments == kat["frames"][name]["segments"]
+    assert rmse < 1e-4 and exact >= 0.999, (name, rmse, exact, mx)
+
+
+SCENES = {
+    "rtow": lambda: scenes.rtow_13_1(96, 60)[:2],
+    "example_sdl": lambda: scenes.example_sdl(96, 60),
+    "quadric_sdl": lambda: scenes.quadric_sdl(80, 80),
+    "cornell": lambda: scenes.cornell_box(64, 64),
+    "cornell_axis_aligned": lambda: scenes.cornell_box(64, 64, rotated=False),
+    "mesh": lambda: scenes.mesh_scene(96, 54, 24, 60),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_frames_match_oracle(gpu, name):
+    cam, world = SCENES[name]()
+    photo = cam.take_photo().samples(16).depth(8).seed(11)
+    img = photo.shot(None, world)
+    ref, rstats = _oracle(world).render(cam.desc, photo.settings(), threads=16)
+    rmse, exact, mx = _cmp(img, ref)
+    assert photo.last_stats.segments == rstats.segments
+    assert rmse < 1e-4 and exact >= 0.999, (name, rmse, exact, mx)
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_world_hit_random_rays(gpu, name):
+    """World::hit records (t1, t2, point, normal, outside, material) on random rays, bit for bit."""
+    cam, world = SCENES[name]()
+    ds = world.device_scene()
+    orc = _oracle(world)
+    rng = np.random.default_rng(5)
+    n = 4096
+    eye = np.array(cam.desc.look_from[:])
+    o = eye + rng.normal(0, 1.0, (n, 3))
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.ascontiguousarray(np.concatenate([o, d, np.zeros((n, 1))], 1))
+    out = np.zeros((n, 13))
+    assert ds.lib.rs_probe_world_hit(ds.handle, rays.ctypes.data, n, 1e-4, float("inf"), out.ctypes.data) == 0
+    bad = 0
+    for i in range(n):
+        r = np.array(orc.world_hit(o[i], d[i]))
+        g = out[i]
+        same = r[0] == g[0] and (r[0] == 0 or (np.array_equal(r[1:9], g[1:9]) and r[11] == g[11] and r[12] == g[12]))
+        bad += 0 if same else 1
+    assert bad == 0, f"{bad}/{n} world-hit mismatches"
+
+
+def test_determinism_batching_and_rows(gpu, monkeypatch):
+    cam, world, _, _ = scenes.rtow_13_1(120, 75)
+    photo = cam.take_photo().samples(9).depth(8).seed(3)
+    a = photo.shot(None, world)
+    b = photo.shot(None, world)
+    assert np.array_equal(a, b)
+    # tiny batches: samples split over many launches, accumulated in sample order
+    monkeypatch.setenv("RS_MAX_BATCH_ITEMS", "5000")
+    cam2, world2, _, _ = scenes.rtow_13_1(120, 75)
+    c = cam2.take_photo().samples(9).depth(8).seed(3).shot(None, world2)
+    assert np.array_equal(a, c)
+    # rows interleaved over 3 "ranks" into one buffer == full frame (painter.rs:248)
+    ds = world.device_scene()
+    out = np.zeros_like(a)
+    for r in range(3):
+        st = photo.rows(r, 0, 3).settings()
+        ds.render(cam.desc, st, out=out)
+    assert np.array_equal(a, out)
+
+
+def test_pixel_mask_and_untouched_rows(gpu):
+    """painter.rs:204-210: pixels the PixelController rejects come back [0,0,0,0]."""
+    cam, world = scenes.example_sdl(64, 40)
+    photo = cam.take_photo().samples(4).depth(8).seed(2)
+    full = photo.shot(None, world)
+    mask = (np.indices((40, 64)).sum(0) % 3 != 0).astype(np.uint8)
+    out, _ = world.device_scene().render(cam.desc, photo.settings(), mask)
+    assert np.all(out[mask == 0] == 0.0)
+    assert np.array_equal(out[mask == 1], full[mask == 1])
+    ref, _ = _oracle(world).render(cam.desc, photo.settings(), threads=8, mask=mask)
+    assert np.array_equal(out, ref)
+
+
+def test_samples_rule_and_zero_samples(gpu):
+    """painter.rs:110-118: N = floor(sqrt(requested))^2; N = 0 gives NaN (0/0) like the reference."""
+    cam, world = scenes.example_sdl(32, 20)
+    p5 = cam.take_photo().samples(5).depth(4).seed(1)
+    p4 = cam.take_photo().samples(4).depth(4).seed(1)
+    assert np.array_equal(p5.shot(None, world), p4.shot(None, world))
+    z = cam.take_photo().samples(0).depth(4).seed(1).shot(None, world)
+    assert np.isnan(z[..., :3]).all() and (z[..., 3] == 1.0).all()
+
+
+def test_render_device_into_torch(gpu):
+    torch = gpu
+    cam, world, _, _ = scenes.rtow_13_1(64, 40)
+    photo = cam.take_photo().samples(4).depth(8).seed(9)
+    host = photo.shot(None, world)
+    t = torch.zeros((40, 64, 4), dtype=torch.float32, device="cuda")
+    st = world.device_scene().render_device(cam.desc, photo.settings(), t.data_ptr(),
+                                            torch.cuda.current_stream().cuda_stream)
+    assert st.launches >= 1 and st.path_ms > 0
+    assert np.array_equal(t.cpu().numpy(), host)
+
+
+def test_bench_config_rows_match_oracle(gpu):
+    """Full bench size (800x500, 64 spp, depth 8): the oracle re-renders every 50th row and those
+    rows must match; size-independent properties on the whole frame."""
+    cam, world, _, _ = scenes.rtow_13_1(800, 500)
+    photo = cam.take_photo().samples(64).depth(8).seed(1)
+    img = photo.shot(None, world)
+    assert np.isfinite(img).all() and (img[..., 3] == 1.0).all()
+    assert photo.last_stats.samples == 800 * 500 * 64
+    st = photo.rows(0, 0, 50).settings()
+    ref, _ = _oracle(world).render(cam.desc, st, threads=16)
+    rmse, exact, mx = _cmp(img[::50], ref[::50])
+    assert rmse < 1e-4 and exact >= 0.999, (rmse, exact, mx)
+
+
+def test_passes_combine_like_cli(gpu):
+    """raysnail.rs:379-427 passes folded with combine_pixel: GPU passes via render_sharded on one
+    device (virtual ranks) == oracle passes folded in numpy."""
+    torch = gpu
+    from raysnail_amd.distributed import combine_pixels
+    cam, world = scenes.example_sdl(48, 30)
+    photo = cam.take_photo().samples(4).depth(8).seed(4)
+    ds = world.device_scene()
+    orc = _oracle(world)
+    acc_t = torch.zeros((30, 48, 4), dtype=torch.float32, device="cuda")
+    acc_t[..., 3] = 1
+    acc_n = np.zeros((30, 48, 4), np.float32)
+    acc_n[..., 3] = 1
+    for p in range(3):
+        st = photo.pass_index(p).settings()
+        g, _ = ds.render(cam.desc, st)
+        r, _ = orc.render(cam.desc, st, threads=8)
+        assert np.array_equal(g, r)
+        acc_t = combine_pixels(acc_t, torch.from_numpy(g).cuda(), float(p))
+        acc_n = (acc_n * np.float32(p) + r) / np.float32(p + 1)
+    assert np.allclose(acc_t.cpu().numpy(), acc_n, rtol=0, atol=1e-6)
