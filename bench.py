@@ -21,8 +21,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-STATE_BYTES_PER_SEGMENT = 212  # extend 28+16, shade 76+16+76
-STATE_BYTES_PER_SAMPLE = 124   # generate 76, finalize 16+32
 
 
 def log(*a):
@@ -42,7 +40,7 @@ def cpu_baseline(cam, world, spp, depth, seed, row_step, threads):
     _, stats = sc.render(cam.desc, st, threads=threads)
     dt = time.perf_counter() - t0
     return {"value": stats.samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"every {row_step}th row of the 800x500x64 frame ({stats.samples} samples, "
+            "sample": f"rows 0::{row_step} of the 800x500x64 frame ({stats.samples} samples, "
                       f"{stats.segments} segments) in {dt:.1f} s, {threads} threads, oracle/oracle.cpp f64"}
 
 
@@ -72,7 +70,7 @@ def main():
     ap.add_argument("--split", choices=["passes", "rows"], default="passes")
     ap.add_argument("--mode", type=int, default=0, help="RS_MODE_* (0 auto)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-row-step", type=int, default=2)
+    ap.add_argument("--cpu-row-step", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
@@ -112,14 +110,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    path_ms = []
+    kern_ms = 0.0
+    kern_launches = 0
+    kern_bytes = 0
     segs = 0
     samples = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         st = last["stats"]
-        path_ms.append(st.path_ms / max(1, st.launches))
+        kern_ms += st.kernel_ms
+        kern_launches += st.kernel_launches
+        kern_bytes += st.kernel_bytes
         segs += st.segments
         samples += st.samples
     torch.cuda.synchronize()
@@ -138,17 +140,20 @@ def main():
     if rank == 0:
         n_eff = int(args.spp ** 0.5) ** 2
         value = all_samples / dt / 1e6
-        # roofline of the dominant kernel (the path-tracing launch), rank 0's launches
-        my_samples_per_launch = samples / max(1, args.steps * max(1, last["stats"].launches))
-        my_segs_per_launch = segs / max(1, args.steps * max(1, last["stats"].launches))
-        alg_bytes = STATE_BYTES_PER_SEGMENT * my_segs_per_launch + STATE_BYTES_PER_SAMPLE * my_samples_per_launch
-        avg_launch_s = sum(path_ms) / len(path_ms) / 1e3
-        achieved = alg_bytes / avg_launch_s / 1e9
+        # roofline of the dominant kernel, rank 0's launches: algorithmic bytes per launch (library
+        # model from the queue counts, DESIGN.md Roofline) / mean event-timed launch duration
+        from raysnail_amd._abi import KERNEL_NAMES
+        kname = KERNEL_NAMES.get(last["stats"].kernel_id)
+        avg_launch_s = kern_ms / max(1, kern_launches) / 1e3
+        bytes_per_launch = kern_bytes / max(1, kern_launches)
+        achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        traffic = load_pmc(kname) if kname else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc("k_path_mega"),
-                "kernel": "k_path_mega", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                "alg_bytes_per_launch": int(alg_bytes),
-                "segments_per_sample": round(my_segs_per_launch / max(1.0, my_samples_per_launch), 4)}
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": kname, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                "alg_bytes_per_launch": int(bytes_per_launch), "launches_per_step": kern_launches // args.steps,
+                "kernel_share_of_step": round(kern_ms / args.steps / (dt / args.steps * 1e3), 4),
+                "segments_per_sample": round(segs / max(1, samples), 4)}
         cpu = None
         if args.cpu_baseline and world == 1:
             log("timing CPU baseline (oracle restatement) ...")

@@ -147,13 +147,21 @@ typedef struct rs_render_settings {
     uint32_t row_step;   /* 0 or 1 = every row */
 } rs_render_settings;
 
+#define RS_KERNEL_NONE       0
+#define RS_KERNEL_PATH_MEGA  1  /* k_path_mega: whole path per thread */
+#define RS_KERNEL_WF_EXTEND  2  /* k_wf_extend: wavefront traversal (generic scenes) */
+#define RS_KERNEL_WFS_EXTEND 3  /* k_wfs_extend: wavefront traversal + material classification */
 typedef struct rs_render_stats {
     uint64_t samples;    /* camera samples traced */
     uint64_t segments;   /* world.hit calls (path segments) */
     double   ms;         /* wall time inside the call (device work + sync) */
-    double   path_ms;    /* device time of the path-tracing launches (HIP events on the call's stream) */
+    double   path_ms;    /* device time of all path-tracing launches (HIP events on the call's stream) */
     uint32_t launches;   /* number of path-tracing launches in the call */
-    uint32_t _pad;
+    uint32_t kernel_launches; /* launches of the dominant kernel (megakernel or wavefront extend) */
+    double   kernel_ms;  /* device time of those launches (HIP events bracketing each launch) */
+    uint64_t kernel_bytes;    /* algorithmic HBM bytes those launches move */
+    int32_t  kernel_id;       /* RS_KERNEL_* */
+    int32_t  _pad;
 } rs_render_stats;
 
 typedef struct rs_scene rs_scene;

@@ -72,7 +72,11 @@ class rs_render_settings(C.Structure):
 
 class rs_render_stats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("ms", C.c_double), ("path_ms", C.c_double),
-                ("launches", C.c_uint32), ("_pad", C.c_uint32)]
+                ("launches", C.c_uint32), ("kernel_launches", C.c_uint32), ("kernel_ms", C.c_double),
+                ("kernel_bytes", C.c_uint64), ("kernel_id", C.c_int32), ("_pad", C.c_int32)]
+
+
+KERNEL_NAMES = {0: None, 1: "k_path_mega", 2: "k_wf_extend", 3: "k_wfs_extend"}
 
 
 D3 = C.c_double * 3

@@ -155,6 +155,13 @@ struct rs_scene {
     unsigned long long* d_cnt = nullptr;
     uint8_t* d_mask = nullptr; size_t mask_cap = 0;
     float* d_out = nullptr; size_t out_cap = 0;
+    // wavefront path state (capacity wf_cap paths) + per-chunk queue counters
+    void* d_wf = nullptr; size_t wf_cap = 0;
+    uint32_t* d_counts = nullptr; size_t counts_cap = 0;
+    uint64_t wf_chunk = 32ull << 20;              // RS_WF_CHUNK overrides
+    int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
+    uint32_t** d_qptrs = nullptr;                 // device array of the per-class queues
+    uint32_t* qptr[kWfsClasses] = {nullptr};
     uint64_t max_items_per_batch = 32ull << 20;  // RS_MAX_BATCH_ITEMS overrides (tests)
     int tree_depth = 0;
     double time0 = 0.0, time1 = 0.0;        // World::new time_limit (world.rs:40-53)
@@ -169,6 +176,9 @@ struct rs_scene {
         if (d_cnt) (void)hipFree(d_cnt);
         if (d_mask) (void)hipFree(d_mask);
         if (d_out) (void)hipFree(d_out);
+        if (d_wf) (void)hipFree(d_wf);
+        if (d_counts) (void)hipFree(d_counts);
+        d_wf = nullptr; d_counts = nullptr; wf_cap = counts_cap = 0;
         d_rad = d_acc = nullptr; d_cnt = nullptr; d_mask = nullptr; d_out = nullptr;
         rad_cap = acc_cap = mask_cap = out_cap = 0;
     }
@@ -285,10 +295,36 @@ struct rs_scene {
 namespace {
 
 // ---------------------------------------------------------------- BVH (binned SAH) ----
+// host-side node with exact f64 child boxes; converted to the f32 device node at upload
+struct HNode {
+    double lo[2][3];
+    double hi[2][3];
+    int32_t child[2];
+};
+float round_down_f(double x) {
+    if (std::isnan(x)) return (float)x;
+    float f = (float)x;
+    return ((double)f > x) ? std::nextafter(f, -INFINITY) : f;
+}
+float round_up_f(double x) {
+    if (std::isnan(x)) return (float)x;
+    float f = (float)x;
+    return ((double)f < x) ? std::nextafter(f, INFINITY) : f;
+}
+DNode to_device(const HNode& h) {
+    DNode d;
+    std::memset(&d, 0, sizeof(d));
+    for (int c = 0; c < 2; ++c)
+        for (int k = 0; k < 3; ++k) { d.lo[c][k] = round_down_f(h.lo[c][k]); d.hi[c][k] = round_up_f(h.hi[c][k]); }
+    d.child[0] = h.child[0];
+    d.child[1] = h.child[1];
+    return d;
+}
+
 struct BuildItem { Box3 box; double c[3]; int32_t prim; };
 
 struct Builder {
-    std::vector<DNode> nodes;
+    std::vector<HNode> nodes;
     int max_depth = 0;
     static double area(const Box3& b) {
         double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
@@ -340,7 +376,7 @@ struct Builder {
         Box3 lb, rb;
         const int32_t l = build(it, b, mid, depth + 1, lb);
         const int32_t r = build(it, mid, e, depth + 1, rb);
-        DNode& n = nodes[idx];
+        HNode& n = nodes[idx];
         std::memset(&n, 0, sizeof(n));
         for (int k = 0; k < 3; ++k) { n.lo[0][k] = lb.lo[k]; n.hi[0][k] = lb.hi[k]; n.lo[1][k] = rb.lo[k]; n.hi[1][k] = rb.hi[k]; }
         n.child[0] = l; n.child[1] = r;
@@ -353,7 +389,7 @@ struct Builder {
 // axis and one object per leaf: the tree the CPU oracle builds, so reference-order traversal
 // visits objects in the same sequence as the oracle's recursion.
 struct RefItem { Box3 box; double key_lo[3]; int32_t prim; };
-int32_t build_ref(std::vector<DNode>& nodes, std::vector<RefItem>& it, size_t b, size_t e, int depth, int& max_depth,
+int32_t build_ref(std::vector<HNode>& nodes, std::vector<RefItem>& it, size_t b, size_t e, int depth, int& max_depth,
                   Box3& out) {
     if (e - b == 1) { out = it[b].box; return ~it[b].prim; }
     max_depth = std::max(max_depth, depth + 1);
@@ -371,7 +407,7 @@ int32_t build_ref(std::vector<DNode>& nodes, std::vector<RefItem>& it, size_t b,
     Box3 lb, rb;
     const int32_t l = build_ref(nodes, it, b, mid, depth + 1, max_depth, lb);
     const int32_t r = build_ref(nodes, it, mid, e, depth + 1, max_depth, rb);
-    DNode& n = nodes[idx];
+    HNode& n = nodes[idx];
     std::memset(&n, 0, sizeof(n));
     for (int k = 0; k < 3; ++k) { n.lo[0][k] = lb.lo[k]; n.hi[0][k] = lb.hi[k]; n.lo[1][k] = rb.lo[k]; n.hi[1][k] = rb.hi[k]; }
     n.child[0] = l; n.child[1] = r;
@@ -527,7 +563,7 @@ void commit(rs_scene* s) {
             code = B.build(items, 0, items.size(), 0, rb);
         }
         if (code < 0) {  // a single object: wrap it in one node (second slot empty)
-            DNode n;
+            HNode n;
             std::memset(&n, 0, sizeof(n));
             for (int k = 0; k < 3; ++k) { n.lo[0][k] = rb.lo[k]; n.hi[0][k] = rb.hi[k]; n.lo[1][k] = INFINITY; n.hi[1][k] = -INFINITY; }
             n.child[0] = code; n.child[1] = INT32_MIN;
@@ -544,7 +580,15 @@ void commit(rs_scene* s) {
     std::vector<int32_t> lights(s->lights.begin(), s->lights.end());
     DScene& d = s->ds;
     std::memset(&d, 0, sizeof(d));
-    d.nodes = upload(s, B.nodes);
+    std::vector<DNode> dnodes;
+    for (const HNode& h : B.nodes) dnodes.push_back(to_device(h));
+    std::vector<DBox64> pboxes(s->objs.size());
+    for (size_t h = 0; h < s->objs.size(); ++h) {
+        const Box3 b = s->bbox((uint32_t)h);
+        for (int k = 0; k < 3; ++k) { pboxes[h].lo[k] = b.lo[k]; pboxes[h].hi[k] = b.hi[k]; }
+    }
+    d.nodes = upload(s, dnodes);
+    d.pbox = upload(s, pboxes);
     d.prims = upload(s, prims);
     d.spheres = upload(s, spheres);
     d.rects = upload(s, rects);
@@ -619,6 +663,39 @@ void ensure(T*& p, size_t& cap, size_t n) {
     cap = n;
 }
 
+WfState carve_wf(rs_scene* s, uint64_t cap) {
+    const size_t per_set = 4 * sizeof(D4) + sizeof(uint4) + sizeof(uint32_t);
+    const size_t per = 2 * per_set + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
+    if (cap > s->wf_cap) {
+        if (s->d_wf) HIP_OK(hipFree(s->d_wf));
+        s->d_wf = nullptr;
+        HIP_OK(hipMalloc(&s->d_wf, per * cap + 8192));
+        s->wf_cap = cap;
+    }
+    char* p = (char*)s->d_wf;
+    const uint64_t c = s->wf_cap;
+    WfState w;
+    for (int k = 0; k < 2; ++k) {
+        WfSet& t = w.set[k];
+        t.ray_o = (D4*)p; p += sizeof(D4) * c;
+        t.ray_d = (D4*)p; p += sizeof(D4) * c;
+        t.thr = (D4*)p; p += sizeof(D4) * c;
+        t.rad = (D4*)p; p += sizeof(D4) * c;
+        t.rng = (uint4*)p; p += sizeof(uint4) * c;
+        t.item = (uint32_t*)p; p += sizeof(uint32_t) * c;
+        p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+    }
+    w.hit = (double2*)p; p += sizeof(double2) * c;
+    uint32_t* qp[kWfsClasses];
+    for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p += sizeof(uint32_t) * c; }
+    p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+    s->d_qptrs = (uint32_t**)p;
+    HIP_OK(hipMemcpy(s->d_qptrs, qp, sizeof(qp), hipMemcpyHostToDevice));
+    for (int k = 0; k < kWfsClasses; ++k) s->qptr[k] = qp[k];
+    w.counts = nullptr;
+    return w;
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -633,12 +710,13 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
     if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
     if (!cam || !st || !d_out) throw Error(RS_E_INVALID, "null argument");
     if (cam->width == 0 || cam->height == 0) throw Error(RS_E_INVALID, "empty image");
-    if (st->mode == RS_MODE_WAVEFRONT) throw Error(RS_E_UNSUPPORTED, "wavefront mode not built yet");
+    if (st->mode < RS_MODE_AUTO || st->mode > RS_MODE_WAVEFRONT) throw Error(RS_E_INVALID, "unknown render mode");
+    const bool wavefront = st->mode != RS_MODE_MEGAKERNEL;
     const uint32_t W = cam->width, H = cam->height;
     const uint32_t rb = st->row_begin;
     const uint32_t re = st->row_end ? std::min(st->row_end, H) : H;
     const uint32_t rstep = st->row_step ? st->row_step : 1;
-    if (rb >= re) { if (stats) *stats = rs_render_stats{0, 0, 0.0, 0.0, 0, 0}; return; }
+    if (rb >= re) { if (stats) *stats = rs_render_stats{0, 0, 0.0, 0.0, 0, 0, 0.0, 0, 0, 0}; return; }
     const uint32_t n_rows = (re - rb + rstep - 1) / rstep;
     const uint64_t n_pix64 = (uint64_t)n_rows * W;
     if (n_pix64 > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "frame too large");
@@ -659,18 +737,79 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
     if (spb) ensure(s->d_rad, s->rad_cap, (size_t)3 * n_pix * spb);
 
     const uint32_t n_batches = spb ? (N + spb - 1) / spb : 0;
-    std::vector<hipEvent_t> ev(2 * (size_t)n_batches);
+    const uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(s->wf_chunk, (uint64_t)n_pix * std::max(spb, 1u)));
+    uint64_t n_chunks_total = 0;
+    for (uint32_t s0 = 0; s0 < N; s0 += spb) n_chunks_total += ((uint64_t)n_pix * std::min(spb, N - s0) + chunk - 1) / chunk;
+    WfState WS{};
+    const bool sorted = wavefront && s->spheres_only;   // material-sorted shading (spheres-only scenes)
+    const uint32_t cstride = sorted ? kWfsStride : 1;
+    if (wavefront && N > 0) {
+        WS = carve_wf(s, chunk);
+        const size_t nc = (size_t)n_chunks_total * (st->depth + 1) * cstride;
+        ensure(s->d_counts, s->counts_cap, nc);
+        WS.counts = s->d_counts;
+        if (!s->n_cu) {
+            hipDeviceProp_t prop;
+            HIP_OK(hipGetDeviceProperties(&prop, s->device));
+            s->n_cu = prop.multiProcessorCount;
+            HIP_OK(wf_occupancy(s->spheres_only, &s->ext_bpc, &s->shade_bpc));
+        }
+    }
+    const size_t n_kernel_ev = wavefront ? (size_t)n_chunks_total * st->depth : n_batches;
+    std::vector<hipEvent_t> ev(2 * (size_t)n_batches), kev(2 * n_kernel_ev);
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
+    for (auto& e : kev) HIP_OK(hipEventCreate(&e));
     auto t0 = std::chrono::steady_clock::now();
     HIP_OK(hipMemsetAsync(s->d_cnt, 0, 512 * sizeof(unsigned long long), stream));
+    if (wavefront && N > 0)
+        HIP_OK(hipMemsetAsync(s->d_counts, 0, (size_t)n_chunks_total * (st->depth + 1) * cstride * sizeof(uint32_t), stream));
     if (N == 0) HIP_OK(hipMemsetAsync(s->d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
     uint32_t bi = 0;
+    size_t ki = 0;
+    uint64_t chunk_i = 0;
+    uint32_t path_launches = 0;
+    const uint32_t ext_blocks = (uint32_t)std::max(1, s->n_cu * std::max(1, s->ext_bpc));
+    const uint32_t shade_blocks = (uint32_t)std::max(1, s->n_cu * std::max(1, s->shade_bpc));
     for (uint32_t s0 = 0; s0 < N; s0 += spb, ++bi) {
         const uint32_t nb = std::min(spb, N - s0);
         pp.s0 = s0;
         pp.n_items = (uint64_t)n_pix * nb;
         HIP_OK(hipEventRecord(ev[2 * bi], stream));
-        HIP_OK(launch_path_mega(s->ds, dc, pp, s->spheres_only, s->d_rad, s->d_cnt, stream));
+        if (!wavefront) {
+            HIP_OK(hipEventRecord(kev[2 * ki], stream));
+            HIP_OK(launch_path_mega(s->ds, dc, pp, s->spheres_only, s->d_rad, s->d_cnt, stream));
+            HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
+            ++ki;
+            ++path_launches;
+        } else {
+            for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i) {
+                const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, pp.n_items - c0);
+                WS.counts = s->d_counts + chunk_i * (st->depth + 1) * cstride;
+                HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, s->d_rad, stream));
+                ++path_launches;
+                const uint32_t wide = (uint32_t)(s->n_cu * 8);
+                for (uint32_t b = 0; sorted && b < st->depth; ++b) {
+                    HIP_OK(hipEventRecord(kev[2 * ki], stream));
+                    HIP_OK(launch_wfs_extend(s->ds, WS, s->d_qptrs, b, cstride, pp.n_items, s->d_rad,
+                                             std::min(wide, (n + kBlock - 1) / kBlock), stream));
+                    HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
+                    ++ki;
+                    for (int k = 0; k < kWfsClasses; ++k)
+                        HIP_OK(launch_wfs_shade(s->ds, WS, s->qptr[k], k, b, cstride, st->depth, pp.n_items, s->d_rad,
+                                                std::min(wide, (n + kBlock - 1) / kBlock), stream));
+                    path_launches += 1 + kWfsClasses;
+                }
+                for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
+                    HIP_OK(hipEventRecord(kev[2 * ki], stream));
+                    HIP_OK(launch_wf_extend(s->ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock), s->spheres_only, stream));
+                    HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
+                    ++ki;
+                    HIP_OK(launch_wf_shade(s->ds, WS, b, st->depth, pp.n_items, s->d_rad,
+                                           std::min(shade_blocks, (n + kBlock - 1) / kBlock), s->spheres_only, stream));
+                    path_launches += 2;
+                }
+            }
+        }
         HIP_OK(hipEventRecord(ev[2 * bi + 1], stream));
         HIP_OK(launch_accumulate(s->d_rad, s->d_acc, n_pix, nb, s0 == 0, stream));
     }
@@ -680,6 +819,9 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
     HIP_OK(launch_finalize(s->d_acc, d_out, fp, stream));
     unsigned long long cnt[512];
     HIP_OK(hipMemcpyAsync(cnt, s->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, stream));
+    const uint32_t cstride_f = (wavefront && s->spheres_only) ? kWfsStride : 1;
+    std::vector<uint32_t> qc(wavefront && N > 0 ? (size_t)n_chunks_total * (st->depth + 1) * cstride_f : 0);
+    if (!qc.empty()) HIP_OK(hipMemcpyAsync(qc.data(), s->d_counts, qc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     auto t1 = std::chrono::steady_clock::now();
     double path_ms = 0.0;
@@ -688,12 +830,47 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
         HIP_OK(hipEventElapsedTime(&ms, ev[2 * b], ev[2 * b + 1]));
         path_ms += ms;
     }
+    double kernel_ms = 0.0;
+    for (size_t k = 0; k < ki; ++k) {
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, kev[2 * k], kev[2 * k + 1]));
+        kernel_ms += ms;
+    }
     for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& e : kev) (void)hipEventDestroy(e);
     if (stats) {
         stats->path_ms = path_ms;
-        stats->launches = n_batches;
+        stats->launches = path_launches;
+        stats->kernel_launches = (uint32_t)ki;
+        stats->kernel_ms = kernel_ms;
         uint64_t seg = 0;
         for (int i = 0; i < 256; ++i) seg += cnt[i];
+        uint64_t cont = 0;
+        if (!qc.empty()) {  // segments = sum over bounces of the extend queue lengths
+            seg = 0;
+            for (uint64_t c = 0; c < n_chunks_total; ++c)
+                for (uint32_t b = 0; b < st->depth; ++b) {
+                    const uint32_t* q = &qc[(c * (st->depth + 1) + b) * cstride_f];
+                    seg += q[0];
+                    if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cont += q[1 + k];
+                }
+        }
+        // algorithmic bytes of the dominant kernel (DESIGN.md Roofline):
+        //  megakernel   : radiance out, 3 x f64 per sample
+        //  wf extend    : ray in (2 x 32 B records) + hit out (16 B) per segment
+        //  wfs extend   : ray in (64 B) per segment; + hit (16 B) + queue slot (4 B) per shaded
+        //                 segment; + throughput/radiance records in (64 B), item (4 B) and radiance
+        //                 out (24 B) per path ending in extend (sky miss / light hit)
+        if (!wavefront) {
+            stats->kernel_id = RS_KERNEL_PATH_MEGA;
+            stats->kernel_bytes = 24ull * (uint64_t)n_pix * N;
+        } else if (cstride_f > 1) {
+            stats->kernel_id = RS_KERNEL_WFS_EXTEND;
+            stats->kernel_bytes = 64ull * seg + 20ull * cont + 92ull * (seg - cont);
+        } else {
+            stats->kernel_id = RS_KERNEL_WF_EXTEND;
+            stats->kernel_bytes = 80ull * seg;
+        }
         stats->segments = seg;
         stats->samples = (uint64_t)n_pix * N;  // masked-out pixels included (they trace nothing)
         stats->ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -739,6 +916,10 @@ int rs_scene_create(rs_scene** out) {
     return run([&] {
         if (!out) throw Error(RS_E_INVALID, "null");
         rs_scene* s = new rs_scene();
+        if (const char* e = std::getenv("RS_WF_CHUNK")) {
+            const unsigned long long v = std::strtoull(e, nullptr, 10);
+            if (v) s->wf_chunk = v;
+        }
         if (const char* e = std::getenv("RS_MAX_BATCH_ITEMS")) {
             const unsigned long long v = std::strtoull(e, nullptr, 10);
             if (v) s->max_items_per_batch = v;

@@ -22,6 +22,26 @@ struct PathParams {
     const uint8_t* mask;    // device, W*H or null
 };
 
+// 32-byte path-state record (one wave load = 2 KiB contiguous)
+struct alignas(32) D4 { double x, y, z, w; };
+
+// Wavefront path state (capacity = chunk size). 32-byte records per path per array, in two
+// ping-pong sets: bounce b reads set b&1 at [0, counts[b]) and the survivors are written,
+// compacted, into set (b+1)&1, so every kernel streams contiguous records.
+struct WfSet {
+    D4* ray_o;            // origin xyz + time
+    D4* ray_d;            // direction xyz
+    D4* thr;              // throughput
+    D4* rad;              // radiance so far
+    uint4* rng;           // XorShift128 state
+    uint32_t* item;       // batch item (sample, pixel) of the path
+};
+struct WfState {
+    WfSet set[2];
+    double2* hit;         // per compacted slot of the current bounce: (prim as bits, accepted range end)
+    uint32_t* counts;     // [depth + 1] live paths per bounce
+};
+
 struct FinalParams {
     uint32_t n_pix_local, width, row_begin, row_step;
     uint32_t n_samples;
@@ -32,6 +52,20 @@ struct FinalParams {
 // Megakernel: one thread per (pixel, sample) path; radiance -> rad[c * n_items + item].
 hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, bool spheres_only, double* rad,
                             unsigned long long* seg_counters, hipStream_t st);
+hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
+                         hipStream_t st);
+hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, bool so, hipStream_t st);
+hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
+                           uint32_t blocks, bool so, hipStream_t st);
+// material-sorted variant (spheres-only scenes): counts stride per bounce = kWfsStride
+constexpr int kWfsClasses = 5;
+constexpr uint32_t kWfsStride = 8;
+hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
+                            uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);
+hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+                           uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);
+// blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
+hipError_t wf_occupancy(bool so, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
 hipError_t launch_probe_hit(const DScene& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
                             hipStream_t st);
 // acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic).

@@ -15,32 +15,90 @@ namespace rs {
 
 // aabb.rs:20-38 with inv = 1/d[i] precomputed per ray (the reference recomputes the same value
 // per node). Branch-free form: max/min over the three axes is equivalent to the early-exit loop
-// because t_min only grows and t_max only shrinks. Returns the entry distance in `entry`.
-__device__ __forceinline__ bool slab(const double lo[3], const double hi[3], const V3& o, const V3& inv, double tmin,
-                                     double tmax, double& entry) {
+// because t_min only grows and t_max only shrinks. This exact f64 test is applied to every
+// object's own bbox before the object is intersected.
+__device__ __forceinline__ bool slab64(const double lo[3], const double hi[3], const V3& o, const V3& inv, double tmin,
+                                       double tmax) {
     double t0x = (lo[0] - o.x) * inv.x, t1x = (hi[0] - o.x) * inv.x;
     double t0y = (lo[1] - o.y) * inv.y, t1y = (hi[1] - o.y) * inv.y;
     double t0z = (lo[2] - o.z) * inv.z, t1z = (hi[2] - o.z) * inv.z;
     if (inv.x < 0.0) { double t = t0x; t0x = t1x; t1x = t; }
     if (inv.y < 0.0) { double t = t0y; t0y = t1y; t1y = t; }
     if (inv.z < 0.0) { double t = t0z; t0z = t1z; t1z = t; }
-    double a = fmax(fmax(fmax(tmin, t0x), t0y), t0z);
-    double b = fmin(fmin(fmin(tmax, t1x), t1y), t1z);
-    entry = a;
+    const double a = fmax(fmax(fmax(tmin, t0x), t0y), t0z);
+    const double b = fmin(fmin(fmin(tmax, t1x), t1y), t1z);
     return !(b <= a);
+}
+
+// Conservative f32 slab test for inner nodes: never rejects a box the exact f64 test of any
+// descendant leaf would accept. Boxes are rounded outward on the host; the ray origin's f32
+// rounding is absorbed by per-axis shifted origins (op = o + d, om = o - d with d >= 4 ulp(o)),
+// the remaining three roundings (inv, sub, mul) by a 2^-18 relative slack on the interval.
+struct RayF {
+    float op[3], om[3], inv[3];
+};
+__device__ __forceinline__ float nextup_f(float f) {  // f finite, not the largest float
+    if (f == 0.0f) return 0x1p-149f;
+    const unsigned u = __float_as_uint(f);
+    return __uint_as_float(f > 0.0f ? u + 1u : u - 1u);
+}
+__device__ __forceinline__ float round_up_f(double x) {
+    const float f = (float)x;
+    return ((double)f < x) ? nextup_f(f) : f;
+}
+__device__ __forceinline__ RayF make_rayf(const V3& o, const V3& inv) {
+    RayF r;
+    const double oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float of = (float)oo[k];
+        const float d = fabsf(of) * 0x1p-20f + 0x1p-126f;
+        r.op[k] = of + d;
+        r.om[k] = of - d;
+        r.inv[k] = (float)ii[k];
+    }
+    return r;
+}
+__device__ __forceinline__ bool slab32(const float lo[3], const float hi[3], const RayF& r, float tmin, float tmax,
+                                       float& entry) {
+    float t0x = (lo[0] - r.op[0]) * r.inv[0], t1x = (hi[0] - r.om[0]) * r.inv[0];
+    float t0y = (lo[1] - r.op[1]) * r.inv[1], t1y = (hi[1] - r.om[1]) * r.inv[1];
+    float t0z = (lo[2] - r.op[2]) * r.inv[2], t1z = (hi[2] - r.om[2]) * r.inv[2];
+    if (r.inv[0] < 0.0f) { float t = t0x; t0x = t1x; t1x = t; }
+    if (r.inv[1] < 0.0f) { float t = t0y; t0y = t1y; t1y = t; }
+    if (r.inv[2] < 0.0f) { float t = t0z; t0z = t1z; t1z = t; }
+    float a = fmaxf(fmaxf(fmaxf(tmin, t0x), t0y), t0z);
+    float b = fminf(fminf(fminf(tmax, t1x), t1y), t1z);
+    a = a - fabsf(a) * 0x1p-18f;
+    b = b + fabsf(b) * 0x1p-18f;
+    entry = a;
+    return a <= b;
 }
 
 // Test one leaf object with the range [tmin, best); on acceptance best := its t1 (the
 // reference's right subtree is searched with `start..left.t1`, bvh.rs:179-188, i.e. the last
 // accepted hit sets the range end, which is the minimum except for Difference's back-face hits).
 template <bool SO>
-__device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, double tmin, double& best, double& bend,
-                                          int& bp) {
+__device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, const V3& inv, double tmin, double& best,
+                                          double& bend, int& bp) {
     const DPrim P = S.prims[p];
     if (SO || P.kind == PK_SPHERE) {
+        const DSphere& sp = S.spheres[P.idx];
+        // the sphere's own bbox, computed exactly as the host did (sphere.rs:117-124; static spheres)
+        double lo[3], hi[3];
+        if (SO || (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0)) {
+            lo[0] = sp.c[0] - sp.r; lo[1] = sp.c[1] - sp.r; lo[2] = sp.c[2] - sp.r;
+            hi[0] = sp.c[0] + sp.r; hi[1] = sp.c[1] + sp.r; hi[2] = sp.c[2] + sp.r;
+        } else {
+            const DBox64& B = S.pbox[p];
+            lo[0] = B.lo[0]; lo[1] = B.lo[1]; lo[2] = B.lo[2]; hi[0] = B.hi[0]; hi[1] = B.hi[1]; hi[2] = B.hi[2];
+        }
+        if (!slab64(lo, hi, r.o, inv, tmin, best)) return;
         double t, t2;
-        if (sphere_t(S.spheres[P.idx], r, tmin, best, t, t2)) { bend = best; best = t; bp = p; }
+        if (sphere_t(sp, r, tmin, best, t, t2)) { bend = best; best = t; bp = p; }
     } else {
+        const DBox64& B = S.pbox[p];
+        if (!slab64(B.lo, B.hi, r.o, inv, tmin, best)) return;
         Hit tmp;
         if (Obj<RS_MAX_NEST>::hit(S, p, r, tmin, best, tmp)) { bend = best; best = tmp.t1; bp = p; }
     }
@@ -56,22 +114,31 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, 
 //    re-read from its parent when popped), so the tests see the same range as BVH::hit.
 // stk: this thread's column of the block's LDS stack (stride kBlock).
 template <bool SO>
-__device__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, int* stk) {
-    if (S.root < 0) return false;
+__device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, int* stk) {
+    if (S.root < 0) return -1;
     const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    const RayF rf = make_rayf(r.o, inv);
+    const float tmin32 = -round_up_f(-tmin);
     double best = RS_INF, bend = RS_INF;
+    float best32 = __builtin_huge_valf();
     int bp = -1;
     int node = S.root;
     int sp = 0;
+#define RS_LEAF(code)                                                          \
+    do {                                                                       \
+        const int bp_prev = bp;                                                \
+        test_leaf<SO>(S, ~(code), r, inv, tmin, best, bend, bp);               \
+        if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
+    } while (0)
     if (SO || !S.ref_order) {
         while (true) {
-            const DNode& N = S.nodes[node];
-            double e0, e1;
+            const DNode N = S.nodes[node];
+            float e0, e1;
             const int c0 = N.child[0], c1 = N.child[1];
-            bool h0 = slab(N.lo[0], N.hi[0], r.o, inv, tmin, best, e0);
-            if (h0 && c0 < 0) { h0 = false; test_leaf<SO>(S, ~c0, r, tmin, best, bend, bp); }
-            bool h1 = slab(N.lo[1], N.hi[1], r.o, inv, tmin, best, e1);
-            if (h1 && c1 < 0) { h1 = false; if (c1 != INT32_MIN) test_leaf<SO>(S, ~c1, r, tmin, best, bend, bp); }
+            bool h0 = slab32(N.lo[0], N.hi[0], rf, tmin32, best32, e0);
+            if (h0 && c0 < 0) { h0 = false; RS_LEAF(c0); }
+            bool h1 = slab32(N.lo[1], N.hi[1], rf, tmin32, best32, e1);
+            if (h1 && c1 < 0) { h1 = false; if (c1 != INT32_MIN) RS_LEAF(c1); }
             if (h0 && h1) {
                 int nn = c0, ff = c1;
                 if (e1 < e0) { nn = c1; ff = c0; }
@@ -91,13 +158,13 @@ __device__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, in
     } else {
         bool second = false;  // visiting node's right child (left one already done)
         while (true) {
-            const DNode& N = S.nodes[node];
-            double e;
+            const DNode N = S.nodes[node];
+            float e;
             if (!second) {
                 const int c0 = N.child[0];
-                if (slab(N.lo[0], N.hi[0], r.o, inv, tmin, best, e)) {
+                if (slab32(N.lo[0], N.hi[0], rf, tmin32, best32, e)) {
                     if (c0 < 0) {
-                        test_leaf<SO>(S, ~c0, r, tmin, best, bend, bp);
+                        RS_LEAF(c0);
                     } else {
                         stk[sp * kBlock] = node;  // come back for the right child
                         ++sp;
@@ -107,9 +174,9 @@ __device__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, in
                 }
             }
             const int c1 = N.child[1];
-            if (c1 != INT32_MIN && slab(N.lo[1], N.hi[1], r.o, inv, tmin, best, e)) {
+            if (c1 != INT32_MIN && slab32(N.lo[1], N.hi[1], rf, tmin32, best32, e)) {
                 if (c1 < 0) {
-                    test_leaf<SO>(S, ~c1, r, tmin, best, bend, bp);
+                    RS_LEAF(c1);
                 } else {
                     node = c1;
                     second = false;
@@ -122,13 +189,27 @@ __device__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, in
             second = true;
         }
     }
+#undef RS_LEAF
+    bend_out = bend;
+    return bp;
+}
+
+// Recompute the full record of the winner with the exact range it was accepted under.
+template <bool SO>
+__device__ __forceinline__ bool finish_hit(const DScene& S, int bp, const Ray& r, double tmin, double bend, Hit& h) {
     if (bp < 0) return false;
-    // Recompute the full record of the winner with the exact range it was accepted under.
     if (SO || S.prims[bp].kind == PK_SPHERE) {
         const DPrim P = S.prims[bp];
         return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, bend, h);
     }
     return Obj<RS_MAX_NEST>::hit(S, bp, r, tmin, bend, h);
+}
+
+template <bool SO>
+__device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, int* stk) {
+    double bend;
+    const int bp = traverse<SO>(S, r, tmin, bend, stk);
+    return finish_hit<SO>(S, bp, r, tmin, bend, h);
 }
 
 // camera.rs:94-100
@@ -138,8 +219,125 @@ __device__ __forceinline__ double phong_highlight(V3 dir_to_light, V3 ray_dir, V
     return spec * factor;
 }
 
-// TakePhotoSettings::ray_color (camera.rs:156-255), recursion unrolled into a loop with a
-// running throughput. Returns the radiance of one camera sample.
+// Scatter on a surface material (after MixedMaterial resolution) and the non-skip_pdf sampling
+// of camera.rs:176-247. KIND is the material class when known at compile time (material-sorted
+// wavefront shading) or -1 for a runtime switch. M0 = the hit's material (settings() source),
+// M = the material that scatters. Returns true when the path continues.
+template <int KIND, bool SO>
+__device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, const DMaterial& M0, const DMaterial& M,
+                                              Ray& ray, V3& T, Rng& rng) {
+    const int kind = KIND >= 0 ? KIND : M.kind;
+    float c[3];
+    Pdf pdf;
+    if (kind == RS_MAT_METAL) {  // metal.rs:104-118
+        tex_color(M, h.p, c);
+        V3 rf = reflect_v(ray.d, h.n);
+        if (!(dot(rf, h.n) > 0.0)) return false;
+        T = v3(T.x * (double)c[0], T.y * (double)c[1], T.z * (double)c[2]);
+        ray.o = h.p; ray.d = rf;
+        return true;
+    } else if (kind == RS_MAT_DIELECTRIC) {  // dielectric.rs:55-93
+        V3 nd;
+        double cos_theta = dot(-ray.d, h.n);
+        double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+        double refr = h.outside ? M.enter_refractive : M.outer_refractive;
+        bool refracted = false;
+        if (!(refr * sin_theta > 1.0)) {
+            double reflect_prob = 0.0;
+            if (M.glass) {  // Glass::reflect_prob, powi(5) = x * ((x*x)*(x*x))
+                double r0 = (1.0 - refr) / (1.0 + refr);
+                r0 = r0 * r0;
+                double x = 1.0 - cos_theta;
+                double x2 = x * x;
+                reflect_prob = fma(1.0 - r0, x * (x2 * x2), r0);
+            }
+            if (!(rng.gen() < reflect_prob)) {
+                V3 rp = (ray.d + cos_theta * h.n) * refr;
+                V3 rq = (-sqrt(1.0 - len2(rp))) * h.n;
+                nd = rp + rq;
+                refracted = true;
+            }
+        }
+        if (!refracted) nd = reflect_v(ray.d, h.n);
+        T = v3(T.x * (double)M.even[0], T.y * (double)M.even[1], T.z * (double)M.even[2]);
+        ray.o = h.p; ray.d = nd;
+        return true;
+    } else if (kind == RS_MAT_LAMBERTIAN) {  // lambertian.rs:39-50
+        tex_color(M, h.p, c);
+        pdf.kind = 0;
+        pdf.n = onb_from(h.n);
+    } else if (kind == RS_MAT_DIFFUSE_METAL) {  // metal.rs:54-68
+        tex_color(M, h.p, c);
+        V3 rf = reflect_v(ray.d, h.n);
+        if (!(dot(rf, h.n) > 0.0)) return false;
+        pdf.kind = 1;
+        pdf.exponent = M.exponent;
+        pdf.refl = onb_from(rf);
+        pdf.n = onb_from(h.n);
+    } else {
+        return false;  // DiffuseLight reached through MixedMaterial: scatter None, no emission
+    }
+    // non-skip_pdf branch (camera.rs:194-247)
+    double light_multi = 1.0, pdf_val;
+    Ray nr;
+    nr.time = ray.time;
+    if (rng.gen() < 0.5) {
+        pdf_val = 0.3183098861837907;
+        const uint32_t li = rng.next_u32() % (uint32_t)S.n_lights;  // list.rs:49-52
+        V3 rv;
+        if (SO) rv = Obj<0>::sphere_random(S.spheres[S.prims[S.lights[li]].idx], h.p, rng);
+        else rv = Obj<RS_MAX_NEST>::random(S, S.lights[li], h.p, rng);
+        V3 dl = unit(rv);
+        if (M0.phong_factor > 0.0) light_multi += phong_highlight(-dl, ray.d, h.n, M0.phong_exponent, M0.phong_factor);
+        nr.o = ray_at(ray, h.t1 - 0.0002);
+        nr.d = dl;
+    } else {
+        V3 sd = (KIND == RS_MAT_LAMBERTIAN) ? onb_local(pdf.n, random_cosine_direction(rng)) : pdf_generate(pdf, rng);
+        pdf_val = pdf_value(pdf, sd);
+        nr.o = h.p;
+        nr.d = sd;
+    }
+    if (pdf_val <= 0.0 || pdf_val != pdf_val) pdf_val = 1e-5;
+    const double mult = pdf_value(pdf, nr.d) / pdf_val;
+    T = v3(((double)c[0] * (light_multi * T.x)) * mult, ((double)c[1] * (light_multi * T.y)) * mult,
+           ((double)c[2] * (light_multi * T.z)) * mult);
+    ray = nr;
+    return true;
+}
+
+// DiffuseLight emission (light.rs:33-35) of the hit's material, as a radiance vector
+__device__ __forceinline__ V3 emission(const DMaterial& M0, V3 p) {
+    float c[3];
+    tex_color(M0, p, c);
+    return v3((double)c[0] * M0.multiplier, (double)c[1] * M0.multiplier, (double)c[2] * M0.multiplier);
+}
+
+// One level of TakePhotoSettings::ray_color (camera.rs:156-255) after world.hit: adds this
+// level's contribution to L and, when the recursion continues, replaces `ray` and multiplies the
+// path throughput T by this level's factor. Returns true when the path continues.
+template <bool SO>
+__device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray, V3& T, V3& L, Rng& rng) {
+    if (!hit_ok) {  // camera.rs:253-254 background
+        V3 bg = background(S, ray);
+        L = L + v3(T.x * bg.x, T.y * bg.y, T.z * bg.z);
+        return false;
+    }
+    const int mi = h.mat >= 0 ? h.mat : S.default_mat;
+    const DMaterial& M0 = S.mats[mi];
+    if (M0.kind == RS_MAT_DIFFUSE_LIGHT) {  // scatter None -> emitted
+        V3 e = emission(M0, h.p);
+        L = L + v3(T.x * e.x, T.y * e.y, T.z * e.z);
+        return false;
+    }
+    int ms = mi;
+    for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {  // mixed_material.rs:43-50
+        const DMaterial& X = S.mats[ms];
+        ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
+    }
+    return shade_surface<-1, SO>(S, h, M0, S.mats[ms], ray, T, rng);
+}
+
+// ray_color iterated: one world.hit per level, at most `depth` levels. Returns the radiance.
 template <bool SO>
 __device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, int* stk, uint32_t& segs) {
     V3 T = v3(1.0, 1.0, 1.0);
@@ -147,102 +345,8 @@ __device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, int
     for (uint32_t d = depth; d > 0; --d) {
         ++segs;
         Hit h;
-        if (!world_hit<SO>(S, ray, 0.0001, h, stk)) {
-            V3 bg = background(S, ray);
-            L = L + v3(T.x * bg.x, T.y * bg.y, T.z * bg.z);
-            break;
-        }
-        const int mi = h.mat >= 0 ? h.mat : S.default_mat;
-        const DMaterial& M0 = S.mats[mi];
-        if (M0.kind == RS_MAT_DIFFUSE_LIGHT) {  // light.rs:33-35, scatter None
-            float c[3];
-            tex_color(M0, h.p, c);
-            V3 e = v3((double)c[0] * M0.multiplier, (double)c[1] * M0.multiplier, (double)c[2] * M0.multiplier);
-            L = L + v3(T.x * e.x, T.y * e.y, T.z * e.z);
-            break;
-        }
-        int ms = mi;
-        for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {  // mixed_material.rs:43-50
-            const DMaterial& X = S.mats[ms];
-            ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
-        }
-        const DMaterial& M = S.mats[ms];
-        float c[3];
-        Pdf pdf;
-        if (M.kind == RS_MAT_METAL) {  // metal.rs:104-118
-            tex_color(M, h.p, c);
-            V3 rf = reflect_v(ray.d, h.n);
-            if (!(dot(rf, h.n) > 0.0)) break;
-            T = v3(T.x * (double)c[0], T.y * (double)c[1], T.z * (double)c[2]);
-            ray.o = h.p; ray.d = rf;
-            continue;
-        } else if (M.kind == RS_MAT_DIELECTRIC) {  // dielectric.rs:55-93
-            V3 nd;
-            double cos_theta = dot(-ray.d, h.n);
-            double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
-            double refr = h.outside ? M.enter_refractive : M.outer_refractive;
-            bool refracted = false;
-            if (!(refr * sin_theta > 1.0)) {
-                double reflect_prob = 0.0;
-                if (M.glass) {  // Glass::reflect_prob, powi(5) = x * ((x*x)*(x*x))
-                    double r0 = (1.0 - refr) / (1.0 + refr);
-                    r0 = r0 * r0;
-                    double x = 1.0 - cos_theta;
-                    double x2 = x * x;
-                    reflect_prob = fma(1.0 - r0, x * (x2 * x2), r0);
-                }
-                if (!(rng.gen() < reflect_prob)) {
-                    V3 rp = (ray.d + cos_theta * h.n) * refr;
-                    V3 rq = (-sqrt(1.0 - len2(rp))) * h.n;
-                    nd = rp + rq;
-                    refracted = true;
-                }
-            }
-            if (!refracted) nd = reflect_v(ray.d, h.n);
-            T = v3(T.x * (double)M.even[0], T.y * (double)M.even[1], T.z * (double)M.even[2]);
-            ray.o = h.p; ray.d = nd;
-            continue;
-        } else if (M.kind == RS_MAT_LAMBERTIAN) {  // lambertian.rs:39-50
-            tex_color(M, h.p, c);
-            pdf.kind = 0;
-            pdf.n = onb_from(h.n);
-        } else if (M.kind == RS_MAT_DIFFUSE_METAL) {  // metal.rs:54-68
-            tex_color(M, h.p, c);
-            V3 rf = reflect_v(ray.d, h.n);
-            if (!(dot(rf, h.n) > 0.0)) break;
-            pdf.kind = 1;
-            pdf.exponent = M.exponent;
-            pdf.refl = onb_from(reflect_v(ray.d, h.n));
-            pdf.n = onb_from(h.n);
-        } else {
-            break;  // DiffuseLight reached through MixedMaterial: scatter None, no emission
-        }
-        // non-skip_pdf branch (camera.rs:194-247)
-        double light_multi = 1.0, pdf_val;
-        Ray nr;
-        nr.time = ray.time;
-        if (rng.gen() < 0.5) {
-            pdf_val = 0.3183098861837907;
-            const uint32_t li = rng.next_u32() % (uint32_t)S.n_lights;  // list.rs:49-52
-            V3 rv;
-            if (SO) rv = Obj<0>::sphere_random(S.spheres[S.prims[S.lights[li]].idx], h.p, rng);
-            else rv = Obj<RS_MAX_NEST>::random(S, S.lights[li], h.p, rng);
-            V3 dl = unit(rv);
-            if (M0.phong_factor > 0.0)
-                light_multi += phong_highlight(-dl, ray.d, h.n, M0.phong_exponent, M0.phong_factor);
-            nr.o = ray_at(ray, h.t1 - 0.0002);
-            nr.d = dl;
-        } else {
-            V3 sd = pdf_generate(pdf, rng);
-            pdf_val = pdf_value(pdf, sd);
-            nr.o = h.p;
-            nr.d = sd;
-        }
-        if (pdf_val <= 0.0 || pdf_val != pdf_val) pdf_val = 1e-5;
-        const double mult = pdf_value(pdf, nr.d) / pdf_val;
-        T = v3(((double)c[0] * (light_multi * T.x)) * mult, ((double)c[1] * (light_multi * T.y)) * mult,
-               ((double)c[2] * (light_multi * T.z)) * mult);
-        ray = nr;
+        const bool ok = world_hit<SO>(S, ray, 0.0001, h, stk);
+        if (!shade_step<SO>(S, ok, h, ray, T, L, rng)) break;
     }
     return L;
 }
@@ -285,6 +389,262 @@ __global__ __launch_bounds__(kBlock) void k_path_mega(DScene S, DCamera C, PathP
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s64 += __shfl_xor(s64, off, 64);
     if ((threadIdx.x & 63) == 0 && s64) atomicAdd(&seg_counters[blockIdx.x & 255], s64);
+}
+
+// ============================================================== wavefront path ====
+// Path state is SoA-of-32-byte-records in HBM (one record per array per path, so a wave's
+// load is 2 KiB contiguous). Bounce b: k_wf_extend traverses every path on queue b and writes
+// (prim, range end); k_wf_shade finishes the record, applies the material and appends the
+// surviving paths to queue b+1 with one atomic per wave (ballot + popcount prefix).
+__device__ __forceinline__ Ray load_ray(const WfSet& W, uint32_t p) {
+    const D4 a = W.ray_o[p], b = W.ray_d[p];
+    Ray r;
+    r.o = v3(a.x, a.y, a.z); r.time = a.w;
+    r.d = v3(b.x, b.y, b.z);
+    return r;
+}
+__device__ __forceinline__ void store_path(const WfSet& W, uint32_t p, const Ray& r, const V3& T, const V3& L,
+                                           const Rng& rng, uint32_t item) {
+    D4 a, b, t, l;
+    a.x = r.o.x; a.y = r.o.y; a.z = r.o.z; a.w = r.time;
+    b.x = r.d.x; b.y = r.d.y; b.z = r.d.z; b.w = 0.0;
+    t.x = T.x; t.y = T.y; t.z = T.z; t.w = 0.0;
+    l.x = L.x; l.y = L.y; l.z = L.z; l.w = 0.0;
+    W.ray_o[p] = a; W.ray_d[p] = b; W.thr[p] = t; W.rad[p] = l;
+    W.rng[p] = make_uint4(rng.x, rng.y, rng.z, rng.w);
+    W.item[p] = item;
+}
+
+// wave-aggregated slot allocation: one atomic per wave, flagged lanes get consecutive slots
+__device__ __forceinline__ uint32_t wave_slot(bool flag, uint32_t* counter) {
+    const unsigned long long m = __ballot(flag);
+    if (m == 0ull) return 0;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// Block-aggregated slot allocation for up to C independent counters: ONE returning atomic per
+// block and counter (a single hot word sustains only ~88 atomics/us, MI355X_MICROARCH.md
+// 'dequeue'), lanes get slots ordered by (wave, lane). Must be called by every thread of the block.
+template <int C>
+__device__ __forceinline__ uint32_t block_slot(int cls, uint32_t* const* counters) {
+    __shared__ uint32_t wcnt[C][kBlock / 64];
+    __shared__ uint32_t bbase[C];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long mine = 0ull;
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        const unsigned long long m = __ballot(cls == k);
+        if (cls == k) mine = m;
+        if (lane == 0) wcnt[k][wave] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < C) {
+        const int k = threadIdx.x;
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) { const uint32_t c = wcnt[k][w]; wcnt[k][w] = tot; tot += c; }
+        bbase[k] = tot ? atomicAdd(counters[k], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t slot = 0;
+    if (cls >= 0 && cls < C) slot = bbase[cls] + wcnt[cls][wave] + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull));
+    __syncthreads();  // wcnt / bbase are reused by the next call
+    return slot;
+}
+__device__ __forceinline__ uint32_t block_slot1(bool flag, uint32_t* counter) {
+    uint32_t* const cs[1] = {counter};
+    return block_slot<1>(flag ? 0 : -1, cs);
+}
+
+// painter.rs:167-170 + camera.rs:77-85 for every (pixel, sample) item of a chunk
+__global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfState W, uint64_t item0, uint32_t n,
+                                                   double* __restrict__ rad) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    bool live = false;
+    Ray r;
+    Rng rng;
+    uint64_t item = 0;
+    if (i < n) {
+        item = item0 + i;
+        const uint32_t pl = (uint32_t)(item % P.n_pix_local);
+        const uint32_t sl = (uint32_t)(item / P.n_pix_local);
+        const uint32_t x = pl % P.width;
+        const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
+        const uint64_t pix = (uint64_t)y * P.width + x;
+        if ((!P.mask || P.mask[pix]) && P.depth > 0) {
+            const uint32_t s = P.s0 + sl;
+            rng.seed_from_u64(splitmix64(splitmix64(P.key_base ^ pix) ^ (uint64_t)s));
+            const uint32_t si = s % P.sqrt_spp, sj = s / P.sqrt_spp;
+            const double sq = (double)P.sqrt_spp;
+            const double xo = (double)x + ((double)si + rng.gen()) / sq;
+            const double yo = (double)y + ((double)sj + rng.gen()) / sq;
+            const double hh = (double)P.height;
+            r = camera_ray(C, xo / (double)P.width, (hh - 1.0 - yo) / hh, rng);
+            live = true;
+        } else {
+            rad[item] = 0.0; rad[P.n_items + item] = 0.0; rad[2 * P.n_items + item] = 0.0;
+        }
+    }
+    const uint32_t slot = block_slot1(live, &W.counts[0]);
+    if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), v3(0.0, 0.0, 0.0), rng, (uint32_t)item);
+}
+
+template <bool SO>
+__global__ __launch_bounds__(kBlock) void k_wf_extend(DScene S, WfState W, uint32_t bounce) {
+    __shared__ int stk_all[kStackMax * kBlock];
+    int* stk = stk_all + threadIdx.x;
+    const uint32_t n = W.counts[bounce];
+    const WfSet& cur = W.set[bounce & 1];
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const Ray r = load_ray(cur, i);
+        double bend = RS_INF;
+        const int bp = traverse<SO>(S, r, 0.0001, bend, stk);
+        W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+    }
+}
+
+template <bool SO>
+__global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32_t bounce, uint32_t depth,
+                                                    uint64_t n_items, double* __restrict__ rad) {
+    const uint32_t n = W.counts[bounce];
+    const WfSet& cur = W.set[bounce & 1];
+    const WfSet& nxt = W.set[(bounce + 1) & 1];
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        bool alive = false;
+        Ray r;
+        V3 T, L;
+        Rng rng;
+        uint32_t item = 0;
+        if (i < n) {
+            r = load_ray(cur, i);
+            const double2 hb = W.hit[i];
+            const int bp = (int)__double_as_longlong(hb.x);
+            Hit h;
+            const bool ok = finish_hit<SO>(S, bp, r, 0.0001, hb.y, h);
+            const D4 t4 = cur.thr[i], l4 = cur.rad[i];
+            T = v3(t4.x, t4.y, t4.z);
+            L = v3(l4.x, l4.y, l4.z);
+            const uint4 g = cur.rng[i];
+            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
+            item = cur.item[i];
+            alive = shade_step<SO>(S, ok, h, r, T, L, rng) && (bounce + 1 < depth);
+            if (!alive) { rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z; }
+        }
+        const uint32_t slot = block_slot1(alive, &W.counts[bounce + 1]);
+        if (alive) store_path(nxt, slot, r, T, L, rng, item);
+    }
+}
+
+// ---- material-sorted wavefront (spheres-only scenes) ----
+// counts layout per bounce: [0] live paths, [1 + k] paths queued for surface class k
+// (k = 0 Lambertian, 1 Metal, 2 DiffuseMetal, 3 Dielectric, 4 other / MixedMaterial).
+// Misses and light hits end in the extend kernel itself (background / emission, camera.rs:172-187,254).
+constexpr int kClasses = 5;
+__device__ __forceinline__ int surface_class(int kind) {
+    return kind == RS_MAT_LAMBERTIAN ? 0 : kind == RS_MAT_METAL ? 1 : kind == RS_MAT_DIFFUSE_METAL ? 2
+         : kind == RS_MAT_DIELECTRIC ? 3 : 4;
+}
+
+__global__ __launch_bounds__(kBlock) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
+                                                      uint32_t bounce, uint32_t stride, uint64_t n_items,
+                                                      double* __restrict__ rad) {
+    __shared__ int stk_all[kStackMax * kBlock];
+    int* stk = stk_all + threadIdx.x;
+    uint32_t* cnt = W.counts + (size_t)bounce * stride;
+    const uint32_t n = cnt[0];
+    const WfSet& cur = W.set[bounce & 1];
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        int cls = -1;
+        if (i < n) {
+            const Ray r = load_ray(cur, i);
+            double bend = RS_INF;
+            const int bp = traverse<true>(S, r, 0.0001, bend, stk);
+            bool done = false;
+            V3 add;
+            if (bp < 0) {
+                add = background(S, r);
+                done = true;
+            } else {
+                const DPrim P = S.prims[bp];
+                const DMaterial& M0 = S.mats[P.mat >= 0 ? P.mat : S.default_mat];
+                if (M0.kind == RS_MAT_DIFFUSE_LIGHT) {
+                    Hit h;
+                    sphere_hit(S.spheres[P.idx], P.mat, r, 0.0001, bend, h);
+                    add = emission(M0, h.p);
+                    done = true;
+                } else {
+                    cls = surface_class(M0.kind);
+                    W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+                }
+            }
+            if (done) {
+                const D4 t4 = cur.thr[i], l4 = cur.rad[i];
+                const uint32_t item = cur.item[i];
+                rad[item] = l4.x + t4.x * add.x;
+                rad[n_items + item] = l4.y + t4.y * add.y;
+                rad[2 * n_items + item] = l4.z + t4.z * add.z;
+            }
+        }
+        uint32_t* const cs[kClasses] = {&cnt[1], &cnt[2], &cnt[3], &cnt[4], &cnt[5]};
+        const uint32_t slot = block_slot<kClasses>(cls, cs);
+        if (cls >= 0) queues[cls][slot] = i;
+    }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const uint32_t* __restrict__ queue,
+                                                     int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
+                                                     uint64_t n_items, double* __restrict__ rad) {
+    const uint32_t* cnt = W.counts + (size_t)bounce * stride;
+    uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
+    const uint32_t n = cnt[1 + cls];
+    const WfSet& cur = W.set[bounce & 1];
+    const WfSet& nxt = W.set[(bounce + 1) & 1];
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t j = base + threadIdx.x;
+        bool alive = false;
+        Ray r;
+        V3 T, L;
+        Rng rng;
+        uint32_t item = 0;
+        if (j < n) {
+            const uint32_t i = queue[j];
+            r = load_ray(cur, i);
+            const double2 hb = W.hit[i];
+            const int bp = (int)__double_as_longlong(hb.x);
+            Hit h;
+            finish_hit<true>(S, bp, r, 0.0001, hb.y, h);
+            const D4 t4 = cur.thr[i], l4 = cur.rad[i];
+            T = v3(t4.x, t4.y, t4.z);
+            L = v3(l4.x, l4.y, l4.z);
+            const uint4 g = cur.rng[i];
+            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
+            item = cur.item[i];
+            const int mi = h.mat >= 0 ? h.mat : S.default_mat;
+            const DMaterial& M0 = S.mats[mi];
+            bool cont;
+            if (KIND >= 0) {
+                cont = shade_surface<KIND, true>(S, h, M0, M0, r, T, rng);
+            } else {
+                int ms = mi;
+                for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {
+                    const DMaterial& X = S.mats[ms];
+                    ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
+                }
+                cont = shade_surface<-1, true>(S, h, M0, S.mats[ms], r, T, rng);
+            }
+            alive = cont && (bounce + 1 < depth);
+            if (!alive) { rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z; }
+        }
+        const uint32_t slot = block_slot1(alive, &cnt_next[0]);
+        if (alive) store_path(nxt, slot, r, T, L, rng, item);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict__ rad, double* __restrict__ acc, uint32_t n_pix,
@@ -357,6 +717,57 @@ hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams&
     else
         hipLaunchKernelGGL(k_path_mega<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s, c, p, rad, seg_counters);
     return hipGetLastError();
+}
+
+hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
+                         hipStream_t st) {
+    const uint32_t blocks = (n + kBlock - 1) / kBlock;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_wf_gen, dim3(blocks), dim3(kBlock), 0, st, c, p, w, item0, n, rad);
+    return hipGetLastError();
+}
+
+hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, bool so, hipStream_t st) {
+    if (so) hipLaunchKernelGGL(k_wf_extend<true>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce);
+    else hipLaunchKernelGGL(k_wf_extend<false>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce);
+    return hipGetLastError();
+}
+
+hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
+                           uint32_t blocks, bool so, hipStream_t st) {
+    if (so) hipLaunchKernelGGL(k_wf_shade<true>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce, depth, n_items, rad);
+    else hipLaunchKernelGGL(k_wf_shade<false>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce, depth, n_items, rad);
+    return hipGetLastError();
+}
+
+hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
+                            uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_wfs_extend, dim3(blocks), dim3(kBlock), 0, st, s, w, queues, bounce, stride, n_items, rad);
+    return hipGetLastError();
+}
+
+hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+                           uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st) {
+    switch (cls) {
+    case 0: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_LAMBERTIAN>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 1: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_METAL>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 2: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_DIFFUSE_METAL>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 3: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_DIELECTRIC>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    default: hipLaunchKernelGGL(k_wfs_shade<-1>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t wf_occupancy(bool so, int* e, int* sh) {
+    hipError_t r;
+    if (so) {
+        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<true>), kBlock, 0);
+        if (r == hipSuccess) r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<true>), kBlock, 0);
+    } else {
+        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<false>), kBlock, 0);
+        if (r == hipSuccess) r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<false>), kBlock, 0);
+    }
+    return r;
 }
 
 hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch, int first_batch,

@@ -86,17 +86,26 @@ struct DMaterial { // src/material/*.rs flattened
     double phong_factor;
 };
 
-// Binary BVH node: both child boxes live in the parent, so one node fetch tests two children.
-// child >= 0: inner node index; child < 0: leaf, prim index = ~child.
-struct alignas(16) DNode {
-    double lo[2][3];
-    double hi[2][3];
+// Binary BVH node: both child boxes live in the parent, so one 64-byte fetch tests two children.
+// child >= 0: inner node index; child < 0: leaf, prim index = ~child; INT32_MIN: empty slot.
+// Boxes are f32 rounded OUTWARD: inner-node tests only cull (conservatively); every leaf is
+// re-tested against the object's exact f64 bbox (DScene::pbox) before the object itself, which
+// is what BVH::hit does with the leaf's own box (bvh.rs:173-177).
+struct alignas(64) DNode {
+    float lo[2][3];
+    float hi[2][3];
     int32_t child[2];
     int32_t pad[2];
 };
 
+struct DBox64 {    // an object's reference bbox (exact f64), tested before its hit()
+    double lo[3];
+    double hi[3];
+};
+
 struct DScene {
     const DNode* nodes;
+    const DBox64* pbox;      // per prim handle
     const DPrim* prims;
     const DSphere* spheres;
     const DRect* rects;

@@ -65,10 +65,11 @@ SCENES = {
 }
 
 
+@pytest.mark.parametrize("mode", [A.RS_MODE_MEGAKERNEL, A.RS_MODE_WAVEFRONT])
 @pytest.mark.parametrize("name", sorted(SCENES))
-def test_frames_match_oracle(gpu, name):
+def test_frames_match_oracle(gpu, name, mode):
     cam, world = SCENES[name]()
-    photo = cam.take_photo().samples(16).depth(8).seed(11)
+    photo = cam.take_photo().samples(16).depth(8).seed(11).mode(mode)
     img = photo.shot(None, world)
     ref, rstats = _oracle(world).render(cam.desc, photo.settings(), threads=16)
     rmse, exact, mx = _cmp(img, ref)
@@ -100,17 +101,23 @@ def test_world_hit_random_rays(gpu, name):
     assert bad == 0, f"{bad}/{n} world-hit mismatches"
 
 
-def test_determinism_batching_and_rows(gpu, monkeypatch):
+@pytest.mark.parametrize("mode", [A.RS_MODE_MEGAKERNEL, A.RS_MODE_WAVEFRONT])
+def test_determinism_batching_and_rows(gpu, monkeypatch, mode):
     cam, world, _, _ = scenes.rtow_13_1(120, 75)
-    photo = cam.take_photo().samples(9).depth(8).seed(3)
+    photo = cam.take_photo().samples(9).depth(8).seed(3).mode(mode)
     a = photo.shot(None, world)
     b = photo.shot(None, world)
     assert np.array_equal(a, b)
     # tiny batches: samples split over many launches, accumulated in sample order
     monkeypatch.setenv("RS_MAX_BATCH_ITEMS", "5000")
     cam2, world2, _, _ = scenes.rtow_13_1(120, 75)
-    c = cam2.take_photo().samples(9).depth(8).seed(3).shot(None, world2)
+    c = cam2.take_photo().samples(9).depth(8).seed(3).mode(mode).shot(None, world2)
     assert np.array_equal(a, c)
+    # tiny wavefront chunks: many chunks per batch
+    monkeypatch.setenv("RS_WF_CHUNK", "3000")
+    cam3, world3, _, _ = scenes.rtow_13_1(120, 75)
+    d = cam3.take_photo().samples(9).depth(8).seed(3).mode(mode).shot(None, world3)
+    assert np.array_equal(a, d)
     # rows interleaved over 3 "ranks" into one buffer == full frame (painter.rs:248)
     ds = world.device_scene()
     out = np.zeros_like(a)
@@ -131,6 +138,17 @@ def test_pixel_mask_and_untouched_rows(gpu):
     assert np.array_equal(out[mask == 1], full[mask == 1])
     ref, _ = _oracle(world).render(cam.desc, photo.settings(), threads=8, mask=mask)
     assert np.array_equal(out, ref)
+
+
+def test_deep_paths_depth50(gpu):
+    """Depth-50 recursion (configs 2-5): wavefront keeps bouncing until every queue drains."""
+    for build in (lambda: scenes.rtow_13_1(40, 25)[:2], lambda: scenes.cornell_box(32, 32)):
+        cam, world = build()
+        photo = cam.take_photo().samples(4).depth(50).seed(8)
+        img = photo.shot(None, world)
+        ref, rs = _oracle(world).render(cam.desc, photo.settings(), threads=16)
+        assert photo.last_stats.segments == rs.segments
+        assert np.array_equal(img, ref)
 
 
 def test_samples_rule_and_zero_samples(gpu):
@@ -157,10 +175,12 @@ def test_render_device_into_torch(gpu):
 
 def test_bench_config_rows_match_oracle(gpu):
     """Full bench size (800x500, 64 spp, depth 8): the oracle re-renders every 50th row and those
-    rows must match; size-independent properties on the whole frame."""
+    rows must match; size-independent properties on the whole frame; both GPU modes agree bitwise."""
     cam, world, _, _ = scenes.rtow_13_1(800, 500)
     photo = cam.take_photo().samples(64).depth(8).seed(1)
     img = photo.shot(None, world)
+    mega = cam.take_photo().samples(64).depth(8).seed(1).mode(A.RS_MODE_MEGAKERNEL).shot(None, world)
+    assert np.array_equal(img, mega)
     assert np.isfinite(img).all() and (img[..., 3] == 1.0).all()
     assert photo.last_stats.samples == 800 * 500 * 64
     st = photo.rows(0, 0, 50).settings()
