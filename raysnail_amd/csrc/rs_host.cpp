@@ -344,7 +344,7 @@ struct Builder {
         double ext = -1;
         for (int k = 0; k < 3; ++k) if (cb.hi[k] - cb.lo[k] > ext) { ext = cb.hi[k] - cb.lo[k]; axis = k; }
         bool done = false;
-        if (depth < 20 && e - b > 2 && ext > 0) {
+        if (depth < 12 && e - b > 2 && ext > 0) {  // SAH near the root, median below: depth <= 12 + log2(n)
             // SAH over a full sweep of the centroid-sorted range on each axis
             double best_cost = INFINITY; int best_axis = -1; size_t best_split = 0;
             std::vector<double> right_area(e - b);
@@ -413,6 +413,62 @@ int32_t build_ref(std::vector<HNode>& nodes, std::vector<RefItem>& it, size_t b,
     n.child[0] = l; n.child[1] = r;
     out = box_union(lb, rb);
     return idx;
+}
+
+// Collapse the binary tree into a 4-wide one: repeatedly open the inner child with the largest
+// box surface until four slots are filled.
+struct HNode4 { double lo[4][3], hi[4][3]; int32_t child[4]; };
+int32_t collapse4(const std::vector<HNode>& bn, int32_t code, std::vector<HNode4>& out, int depth, int& max_depth) {
+    if (code < 0) return code;
+    max_depth = std::max(max_depth, depth + 1);
+    struct Slot { double lo[3], hi[3]; int32_t c; };
+    std::vector<Slot> slots;
+    const HNode& n = bn[code];
+    for (int k = 0; k < 2; ++k) {
+        Slot sl; sl.c = n.child[k];
+        for (int a = 0; a < 3; ++a) { sl.lo[a] = n.lo[k][a]; sl.hi[a] = n.hi[k][a]; }
+        if (sl.c != INT32_MIN) slots.push_back(sl);
+    }
+    while (slots.size() < 4) {
+        int best = -1; double best_area = -1;
+        for (size_t i = 0; i < slots.size(); ++i) {
+            if (slots[i].c < 0) continue;
+            const double dx = slots[i].hi[0] - slots[i].lo[0], dy = slots[i].hi[1] - slots[i].lo[1], dz = slots[i].hi[2] - slots[i].lo[2];
+            const double ar = dx * dy + dy * dz + dz * dx;
+            if (ar > best_area) { best_area = ar; best = (int)i; }
+        }
+        if (best < 0) break;
+        const HNode& m = bn[slots[best].c];
+        Slot a, b;
+        a.c = m.child[0]; b.c = m.child[1];
+        for (int q = 0; q < 3; ++q) { a.lo[q] = m.lo[0][q]; a.hi[q] = m.hi[0][q]; b.lo[q] = m.lo[1][q]; b.hi[q] = m.hi[1][q]; }
+        slots.erase(slots.begin() + best);
+        slots.push_back(a);
+        if (b.c != INT32_MIN) slots.push_back(b);
+    }
+    const int32_t idx = (int32_t)out.size();
+    out.emplace_back();
+    int32_t kids[4];
+    for (int k = 0; k < 4; ++k) kids[k] = (size_t)k < slots.size() ? collapse4(bn, slots[k].c, out, depth + 1, max_depth) : INT32_MIN;
+    HNode4& o = out[idx];
+    for (int k = 0; k < 4; ++k) {
+        o.child[k] = kids[k];
+        for (int q = 0; q < 3; ++q) {
+            o.lo[k][q] = (size_t)k < slots.size() ? slots[k].lo[q] : INFINITY;
+            o.hi[k][q] = (size_t)k < slots.size() ? slots[k].hi[q] : -INFINITY;
+        }
+    }
+    return idx;
+}
+DNode4 to_device4(const HNode4& h) {
+    DNode4 d;
+    std::memset(&d, 0, sizeof(d));
+    for (int k = 0; k < 4; ++k) {
+        d.lo_x[k] = round_down_f(h.lo[k][0]); d.lo_y[k] = round_down_f(h.lo[k][1]); d.lo_z[k] = round_down_f(h.lo[k][2]);
+        d.hi_x[k] = round_up_f(h.hi[k][0]); d.hi_y[k] = round_up_f(h.hi[k][1]); d.hi_z[k] = round_up_f(h.hi[k][2]);
+        d.child[k] = h.child[k];
+    }
+    return d;
 }
 
 template <typename T>
@@ -587,8 +643,29 @@ void commit(rs_scene* s) {
         const Box3 b = s->bbox((uint32_t)h);
         for (int k = 0; k < 3; ++k) { pboxes[h].lo[k] = b.lo[k]; pboxes[h].hi[k] = b.hi[k]; }
     }
+    // wavefront shading class per prim (spheres-only scenes classify by the sphere's material)
+    std::vector<uint8_t> pclass(s->objs.size(), 4);
+    for (size_t h = 0; h < s->objs.size(); ++h) {
+        const int32_t m = s->objs[h].mat >= 0 ? s->objs[h].mat : default_mat;
+        const int k = mats[m].kind;
+        pclass[h] = k == RS_MAT_LAMBERTIAN ? 0 : k == RS_MAT_METAL ? 1 : k == RS_MAT_DIFFUSE_METAL ? 2
+                  : k == RS_MAT_DIELECTRIC ? 3 : k == RS_MAT_DIFFUSE_LIGHT ? 6 : 4;
+    }
     d.nodes = upload(s, dnodes);
     d.pbox = upload(s, pboxes);
+    d.pclass = upload(s, pclass);
+    d.root4 = -1;
+    if (!s->ref_order && root >= 0 && !std::getenv("RS_NO_BVH4")) {
+        std::vector<HNode4> n4;
+        int depth4 = 0;
+        const int32_t r4 = collapse4(B.nodes, root, n4, 0, depth4);
+        if (r4 >= 0 && 3 * depth4 <= kStackMax) {
+            std::vector<DNode4> dn4;
+            for (const HNode4& h : n4) dn4.push_back(to_device4(h));
+            d.nodes4 = upload(s, dn4);
+            d.root4 = r4;
+        }
+    }
     d.prims = upload(s, prims);
     d.spheres = upload(s, spheres);
     d.rects = upload(s, rects);

@@ -7,7 +7,7 @@
 namespace rs {
 
 constexpr int kBlock = 256;      // 4 waves of 64
-constexpr int kStackMax = 32;    // per-thread BVH stack entries (LDS), host enforces tree depth
+constexpr int kStackMax = 24;    // per-thread BVH stack entries (LDS, 24 KiB/block -> 6 blocks/CU); host enforces tree depth
 
 // One batch of camera samples: items = n_pix_local * n_samp_batch, item -> (sample, pixel).
 struct PathParams {
@@ -58,7 +58,7 @@ hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, 
 hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, bool so, hipStream_t st);
 // material-sorted variant (spheres-only scenes): counts stride per bounce = kWfsStride
-constexpr int kWfsClasses = 5;
+constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric, other
 constexpr uint32_t kWfsStride = 8;
 hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);

@@ -31,11 +31,13 @@ __device__ __forceinline__ bool slab64(const double lo[3], const double hi[3], c
 }
 
 // Conservative f32 slab test for inner nodes: never rejects a box the exact f64 test of any
-// descendant leaf would accept. Boxes are rounded outward on the host; the ray origin's f32
-// rounding is absorbed by per-axis shifted origins (op = o + d, om = o - d with d >= 4 ulp(o)),
-// the remaining three roundings (inv, sub, mul) by a 2^-18 relative slack on the interval.
+// descendant leaf would accept. Boxes are rounded outward on the host. The ray origin is shifted
+// per axis by d = |o|*2^-20 + tiny (an expanded box [lo-d, hi+d] in effect), which absorbs the f32
+// rounding of o and of the precomputed products o'*inv (each <= |o| 2^-24); t at a plane is then one
+// FMA, t = lo*inv - (o+d)*inv. The remaining roundings (inv, fma) are relative and covered by a
+// 2^-18 slack on the interval. |inv| is clamped to 1e30 so no inf*0 / inf-inf appears.
 struct RayF {
-    float op[3], om[3], inv[3];
+    float inv[3], opi[3], omi[3];   // inv, (o+d)*inv, (o-d)*inv
 };
 __device__ __forceinline__ float nextup_f(float f) {  // f finite, not the largest float
     if (f == 0.0f) return 0x1p-149f;
@@ -52,25 +54,23 @@ __device__ __forceinline__ RayF make_rayf(const V3& o, const V3& inv) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float of = (float)oo[k];
-        const float d = fabsf(of) * 0x1p-20f + 0x1p-126f;
-        r.op[k] = of + d;
-        r.om[k] = of - d;
-        r.inv[k] = (float)ii[k];
+        const float d = fabsf(of) * 0x1p-20f + 0x1p-100f;
+        const float iv = fminf(fmaxf((float)ii[k], -1e30f), 1e30f);
+        r.inv[k] = iv;
+        r.opi[k] = (of + d) * iv;
+        r.omi[k] = (of - d) * iv;
     }
     return r;
 }
 __device__ __forceinline__ bool slab32(const float lo[3], const float hi[3], const RayF& r, float tmin, float tmax,
                                        float& entry) {
-    float t0x = (lo[0] - r.op[0]) * r.inv[0], t1x = (hi[0] - r.om[0]) * r.inv[0];
-    float t0y = (lo[1] - r.op[1]) * r.inv[1], t1y = (hi[1] - r.om[1]) * r.inv[1];
-    float t0z = (lo[2] - r.op[2]) * r.inv[2], t1z = (hi[2] - r.om[2]) * r.inv[2];
-    if (r.inv[0] < 0.0f) { float t = t0x; t0x = t1x; t1x = t; }
-    if (r.inv[1] < 0.0f) { float t = t0y; t0y = t1y; t1y = t; }
-    if (r.inv[2] < 0.0f) { float t = t0z; t0z = t1z; t1z = t; }
-    float a = fmaxf(fmaxf(fmaxf(tmin, t0x), t0y), t0z);
-    float b = fminf(fminf(fminf(tmax, t1x), t1y), t1z);
-    a = a - fabsf(a) * 0x1p-18f;
-    b = b + fabsf(b) * 0x1p-18f;
+    const float ax = fmaf(lo[0], r.inv[0], -r.opi[0]), bx = fmaf(hi[0], r.inv[0], -r.omi[0]);
+    const float ay = fmaf(lo[1], r.inv[1], -r.opi[1]), by = fmaf(hi[1], r.inv[1], -r.omi[1]);
+    const float az = fmaf(lo[2], r.inv[2], -r.opi[2]), bz = fmaf(hi[2], r.inv[2], -r.omi[2]);
+    float a = fmaxf(fmaxf(fmaxf(tmin, fminf(ax, bx)), fminf(ay, by)), fminf(az, bz));
+    float b = fminf(fminf(fminf(tmax, fmaxf(ax, bx)), fmaxf(ay, by)), fmaxf(az, bz));
+    a = fmaf(-fabsf(a), 0x1p-18f, a);
+    b = fmaf(fabsf(b), 0x1p-18f, b);
     entry = a;
     return a <= b;
 }
@@ -78,26 +78,65 @@ __device__ __forceinline__ bool slab32(const float lo[3], const float hi[3], con
 // Test one leaf object with the range [tmin, best); on acceptance best := its t1 (the
 // reference's right subtree is searched with `start..left.t1`, bvh.rs:179-188, i.e. the last
 // accepted hit sets the range end, which is the minimum except for Difference's back-face hits).
+// Sphere leaf during traversal: same arithmetic as sphere_t (sphere.rs:83-109) with the per-ray
+// a = |d|^2 hoisted and center_at skipped for static spheres (c + 0*t == c bit for bit).
+__device__ __forceinline__ bool sphere_t_trav(const DSphere& s, const Ray& r, double a, double tmin, double tmax,
+                                              double& t) {
+    V3 cc = ld3(s.c);
+    if (s.v[0] != 0.0 || s.v[1] != 0.0 || s.v[2] != 0.0) cc = cc + ld3(s.v) * r.time;
+    const V3 l = r.o - cc;
+    const double half_b = dot(r.d, l);
+    const double c = len2(l) - s.r2;
+    const double delta = half_b * half_b - a * c;
+    if (delta < 0.0) return false;
+    const double sq = sqrt(delta);
+    const double t1 = (-half_b - sq) / a;
+    if (in_range(t1, tmin, tmax)) { t = t1; return true; }
+    const double t2 = (-half_b + sq) / a;
+    if (in_range(t2, tmin, tmax)) { t = t2; return true; }
+    return false;
+}
+
+// Leaf: the object is accepted iff its exact own bbox passes (aabb.rs:20-38, BVH leaf box) AND it
+// hits within [tmin, best). Both are pure, so the cheap test runs first: for spheres the
+// discriminant, and the exact box only for spheres that hit.
 template <bool SO>
-__device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, const V3& inv, double tmin, double& best,
-                                          double& bend, int& bp) {
+__device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, double tmin, double& best, double& bend,
+                                          int& bp) {
     const DPrim P = S.prims[p];
     if (SO || P.kind == PK_SPHERE) {
         const DSphere& sp = S.spheres[P.idx];
-        // the sphere's own bbox, computed exactly as the host did (sphere.rs:117-124; static spheres)
+        const double a_dd = len2(r.d);
+        double t;
+#ifdef RS_ABLATE_LEAF
+        // DIAGNOSTIC ONLY (wrong results): f32 discriminant, no exact box
+        {
+            const float lx = (float)(r.o.x - sp.c[0]), ly = (float)(r.o.y - sp.c[1]), lz = (float)(r.o.z - sp.c[2]);
+            const float hb = (float)r.d.x * lx + (float)r.d.y * ly + (float)r.d.z * lz;
+            const float cc = lx * lx + ly * ly + lz * lz - (float)sp.r2;
+            const float dd = hb * hb - cc;
+            if (dd < 0.0f) return;
+            const float tt = -hb - sqrtf(dd);
+            if (!(tt >= (float)tmin && (double)tt < best)) return;
+            bend = best; best = tt; bp = p;
+            return;
+        }
+#endif
+        if (!sphere_t_trav(sp, r, a_dd, tmin, best, t)) return;
         double lo[3], hi[3];
-        if (SO || (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0)) {
+        if (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0) {  // host: c -/+ r (sphere.rs:117-124)
             lo[0] = sp.c[0] - sp.r; lo[1] = sp.c[1] - sp.r; lo[2] = sp.c[2] - sp.r;
             hi[0] = sp.c[0] + sp.r; hi[1] = sp.c[1] + sp.r; hi[2] = sp.c[2] + sp.r;
         } else {
             const DBox64& B = S.pbox[p];
             lo[0] = B.lo[0]; lo[1] = B.lo[1]; lo[2] = B.lo[2]; hi[0] = B.hi[0]; hi[1] = B.hi[1]; hi[2] = B.hi[2];
         }
+        const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);  // the same value AABB::hit computes
         if (!slab64(lo, hi, r.o, inv, tmin, best)) return;
-        double t, t2;
-        if (sphere_t(sp, r, tmin, best, t, t2)) { bend = best; best = t; bp = p; }
+        bend = best; best = t; bp = p;
     } else {
         const DBox64& B = S.pbox[p];
+        const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
         if (!slab64(B.lo, B.hi, r.o, inv, tmin, best)) return;
         Hit tmp;
         if (Obj<RS_MAX_NEST>::hit(S, p, r, tmin, best, tmp)) { bend = best; best = tmp.t1; bp = p; }
@@ -116,8 +155,7 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, 
 template <bool SO>
 __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, int* stk) {
     if (S.root < 0) return -1;
-    const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-    const RayF rf = make_rayf(r.o, inv);
+    const RayF rf = make_rayf(r.o, v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z));
     const float tmin32 = -round_up_f(-tmin);
     double best = RS_INF, bend = RS_INF;
     float best32 = __builtin_huge_valf();
@@ -127,10 +165,54 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
 #define RS_LEAF(code)                                                          \
     do {                                                                       \
         const int bp_prev = bp;                                                \
-        test_leaf<SO>(S, ~(code), r, inv, tmin, best, bend, bp);               \
+        test_leaf<SO>(S, ~(code), r, tmin, best, bend, bp);                    \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
-    if (SO || !S.ref_order) {
+    if (S.root4 >= 0) {
+        // 4-wide near-first: test the four child boxes of one 128-byte node, leaves at once, inner
+        // children ordered by entry distance (nearest next, the rest pushed far-to-near).
+        node = S.root4;
+        while (true) {
+            const DNode4 N = S.nodes4[node];
+            // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
+            // and tested after the four box tests, when the node's registers are dead
+            int n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+            int l0 = INT32_MIN, l1 = INT32_MIN, l2 = INT32_MIN, l3 = INT32_MIN;
+            float e0 = -__builtin_huge_valf(), e1 = e0, e2 = e0, e3 = e0;
+#define RS_SLOT(K, NK, EK, LK)                                                                \
+            {                                                                                 \
+                const float lo[3] = {N.lo_x[K], N.lo_y[K], N.lo_z[K]};                        \
+                const float hi[3] = {N.hi_x[K], N.hi_y[K], N.hi_z[K]};                        \
+                float e;                                                                      \
+                const int c = N.child[K];                                                     \
+                if (c != INT32_MIN && slab32(lo, hi, rf, tmin32, best32, e)) {                \
+                    if (c < 0) { LK = c; } else { NK = c; EK = e; }                           \
+                }                                                                             \
+            }
+            RS_SLOT(0, n0, e0, l0) RS_SLOT(1, n1, e1, l1) RS_SLOT(2, n2, e2, l2) RS_SLOT(3, n3, e3, l3)
+#undef RS_SLOT
+            if (l0 != INT32_MIN) RS_LEAF(l0);
+            if (l1 != INT32_MIN) RS_LEAF(l1);
+            if (l2 != INT32_MIN) RS_LEAF(l2);
+            if (l3 != INT32_MIN) RS_LEAF(l3);
+            const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
+                            (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
+            if (cnt == 0) {
+                if (sp == 0) break;
+                --sp;
+                node = stk[sp * kBlock];
+                continue;
+            }
+            // sort descending by entry (farthest first, not-visited last): 5 compare-swaps
+#define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
+            RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
+#undef RS_CS
+            if (cnt > 1) { stk[sp * kBlock] = n0; ++sp; }
+            if (cnt > 2) { stk[sp * kBlock] = n1; ++sp; }
+            if (cnt > 3) { stk[sp * kBlock] = n2; ++sp; }
+            node = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
+        }
+    } else if (SO || !S.ref_order) {
         while (true) {
             const DNode N = S.nodes[node];
             float e0, e1;
@@ -541,16 +623,17 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32
 }
 
 // ---- material-sorted wavefront (spheres-only scenes) ----
-// counts layout per bounce: [0] live paths, [1 + k] paths queued for surface class k
-// (k = 0 Lambertian, 1 Metal, 2 DiffuseMetal, 3 Dielectric, 4 other / MixedMaterial).
-// Misses and light hits end in the extend kernel itself (background / emission, camera.rs:172-187,254).
-constexpr int kClasses = 5;
-__device__ __forceinline__ int surface_class(int kind) {
-    return kind == RS_MAT_LAMBERTIAN ? 0 : kind == RS_MAT_METAL ? 1 : kind == RS_MAT_DIFFUSE_METAL ? 2
-         : kind == RS_MAT_DIELECTRIC ? 3 : 4;
-}
+// counts layout per bounce: [0] live paths, [1 + k] paths queued for class k (k = 0 Lambertian,
+// 1 Metal, 2 DiffuseMetal, 3 Dielectric, 4 other / MixedMaterial). The class of a hit is a per-prim
+// byte (DScene::pclass) computed at commit; kClsLight marks DiffuseLight prims, whose paths end
+// inside extend like sky misses (no queue, no second gather of the path state).
+constexpr int kClasses = kWfsClasses;
+constexpr int kClsLight = 6;
 
-__global__ __launch_bounds__(kBlock) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
+#ifndef RS_EXT_MIN_WAVES
+#define RS_EXT_MIN_WAVES 1  // 5 forces <=96 VGPRs but spills; measured slower (14.5 vs 13.8 ms)
+#endif
+__global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad) {
     __shared__ int stk_all[kStackMax * kBlock];
@@ -565,22 +648,21 @@ __global__ __launch_bounds__(kBlock) void k_wfs_extend(DScene S, WfState W, uint
             const Ray r = load_ray(cur, i);
             double bend = RS_INF;
             const int bp = traverse<true>(S, r, 0.0001, bend, stk);
-            bool done = false;
             V3 add;
-            if (bp < 0) {
+            bool done = true;
+            if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
                 add = background(S, r);
-                done = true;
             } else {
-                const DPrim P = S.prims[bp];
-                const DMaterial& M0 = S.mats[P.mat >= 0 ? P.mat : S.default_mat];
-                if (M0.kind == RS_MAT_DIFFUSE_LIGHT) {
+                cls = (int)S.pclass[bp];
+                if (cls == kClsLight) {  // DiffuseLight: emitted, scatter None (camera.rs:172-176,250)
+                    const DPrim P = S.prims[bp];
                     Hit h;
                     sphere_hit(S.spheres[P.idx], P.mat, r, 0.0001, bend, h);
-                    add = emission(M0, h.p);
-                    done = true;
+                    add = emission(S.mats[P.mat >= 0 ? P.mat : S.default_mat], h.p);
+                    cls = -1;
                 } else {
-                    cls = surface_class(M0.kind);
                     W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+                    done = false;
                 }
             }
             if (done) {

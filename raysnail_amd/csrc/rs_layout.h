@@ -98,14 +98,25 @@ struct alignas(64) DNode {
     int32_t pad[2];
 };
 
+// 4-wide node (monotone scenes, near-first traversal): SoA child boxes (f32, rounded outward) so one
+// 128-byte fetch tests four children; child codes as in DNode.
+struct alignas(128) DNode4 {
+    float lo_x[4], lo_y[4], lo_z[4];
+    float hi_x[4], hi_y[4], hi_z[4];
+    int32_t child[4];
+    int32_t pad[4];
+};
+
 struct DBox64 {    // an object's reference bbox (exact f64), tested before its hit()
     double lo[3];
     double hi[3];
 };
 
 struct DScene {
-    const DNode* nodes;
+    const DNode* nodes;      // binary tree (reference-order scenes)
+    const DNode4* nodes4;    // 4-wide tree (monotone scenes), root = root4
     const DBox64* pbox;      // per prim handle
+    const uint8_t* pclass;   // per prim handle: wavefront shading class of its material (spheres-only scenes)
     const DPrim* prims;
     const DSphere* spheres;
     const DRect* rects;
@@ -122,6 +133,8 @@ struct DScene {
     int32_t root;            // root child code (node index, or ~prim if a single object, or INT32_MIN if empty)
     int32_t default_mat;     // world.rs:51 Lambertian(Color(1,1,1,1))
     int32_t ref_order;       // 1: traverse in BVH::hit's recursion order (bvh.rs:173-192); 0: near-first
+    int32_t root4;           // root of nodes4 (>= 0) when the 4-wide tree is used, else -1
+    int32_t pad4;
     float bg_lo[4], bg_hi[4];
 };
 
