@@ -668,6 +668,13 @@ void commit(rs_scene* s) {
     }
     d.prims = upload(s, prims);
     d.spheres = upload(s, spheres);
+    if (s->spheres_only) {  // prim-indexed copy: the traversal's leaf test reads it without the DPrim hop
+        std::vector<DSphere> psph(s->objs.size());
+        std::memset(psph.data(), 0, psph.size() * sizeof(DSphere));
+        for (size_t h = 0; h < s->objs.size(); ++h)
+            if (s->objs[h].kind == PK_SPHERE) psph[h] = spheres[prims[h].idx];
+        d.psph = upload(s, psph);
+    }
     d.rects = upload(s, rects);
     d.boxes = upload(s, boxes);
     d.quadrics = upload(s, quads);

@@ -97,43 +97,37 @@ __device__ __forceinline__ bool sphere_t_trav(const DSphere& s, const Ray& r, do
     return false;
 }
 
+// Sphere leaf: discriminant first, then the exact own box for spheres that hit.
+__device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int p, const Ray& r, double tmin,
+                                                 double& best, double& bend, int& bp) {
+    double t;
+    if (!sphere_t_trav(sp, r, len2(r.d), tmin, best, t)) return;
+    double lo[3], hi[3];
+    if (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0) {  // host: c -/+ r (sphere.rs:117-124)
+        lo[0] = sp.c[0] - sp.r; lo[1] = sp.c[1] - sp.r; lo[2] = sp.c[2] - sp.r;
+        hi[0] = sp.c[0] + sp.r; hi[1] = sp.c[1] + sp.r; hi[2] = sp.c[2] + sp.r;
+    } else {
+        const DBox64& B = S.pbox[p];
+        lo[0] = B.lo[0]; lo[1] = B.lo[1]; lo[2] = B.lo[2]; hi[0] = B.hi[0]; hi[1] = B.hi[1]; hi[2] = B.hi[2];
+    }
+    const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);  // the same value AABB::hit computes
+    if (!slab64(lo, hi, r.o, inv, tmin, best)) return;
+    bend = best; best = t; bp = p;
+}
+
 // Leaf: the object is accepted iff its exact own bbox passes (aabb.rs:20-38, BVH leaf box) AND it
 // hits within [tmin, best). Both are pure, so the cheap test runs first: for spheres the
 // discriminant, and the exact box only for spheres that hit.
 template <bool SO>
 __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, double tmin, double& best, double& bend,
                                           int& bp) {
+    if (SO) {  // prim-indexed sphere copy: one dependent load fewer than prims[p] -> spheres[idx]
+        test_sphere_leaf(S, S.psph[p], p, r, tmin, best, bend, bp);
+        return;
+    }
     const DPrim P = S.prims[p];
-    if (SO || P.kind == PK_SPHERE) {
-        const DSphere& sp = S.spheres[P.idx];
-        const double a_dd = len2(r.d);
-        double t;
-#ifdef RS_ABLATE_LEAF
-        // DIAGNOSTIC ONLY (wrong results): f32 discriminant, no exact box
-        {
-            const float lx = (float)(r.o.x - sp.c[0]), ly = (float)(r.o.y - sp.c[1]), lz = (float)(r.o.z - sp.c[2]);
-            const float hb = (float)r.d.x * lx + (float)r.d.y * ly + (float)r.d.z * lz;
-            const float cc = lx * lx + ly * ly + lz * lz - (float)sp.r2;
-            const float dd = hb * hb - cc;
-            if (dd < 0.0f) return;
-            const float tt = -hb - sqrtf(dd);
-            if (!(tt >= (float)tmin && (double)tt < best)) return;
-            bend = best; best = tt; bp = p;
-            return;
-        }
-#endif
-        if (!sphere_t_trav(sp, r, a_dd, tmin, best, t)) return;
-        double lo[3], hi[3];
-        if (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0) {  // host: c -/+ r (sphere.rs:117-124)
-            lo[0] = sp.c[0] - sp.r; lo[1] = sp.c[1] - sp.r; lo[2] = sp.c[2] - sp.r;
-            hi[0] = sp.c[0] + sp.r; hi[1] = sp.c[1] + sp.r; hi[2] = sp.c[2] + sp.r;
-        } else {
-            const DBox64& B = S.pbox[p];
-            lo[0] = B.lo[0]; lo[1] = B.lo[1]; lo[2] = B.lo[2]; hi[0] = B.hi[0]; hi[1] = B.hi[1]; hi[2] = B.hi[2];
-        }
-        const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);  // the same value AABB::hit computes
-        if (!slab64(lo, hi, r.o, inv, tmin, best)) return;
-        bend = best; best = t; bp = p;
+    if (P.kind == PK_SPHERE) {
+        test_sphere_leaf(S, S.spheres[P.idx], p, r, tmin, best, bend, bp);
     } else {
         const DBox64& B = S.pbox[p];
         const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
@@ -179,38 +173,44 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
             int n0 = 0, n1 = 0, n2 = 0, n3 = 0;
             int l0 = INT32_MIN, l1 = INT32_MIN, l2 = INT32_MIN, l3 = INT32_MIN;
             float e0 = -__builtin_huge_valf(), e1 = e0, e2 = e0, e3 = e0;
+#define RS_SLOT_BODY(c, NK, EK, LK)                                                           \
+                if (c != INT32_MIN && slab32(lo, hi, rf, tmin32, best32, e)) {                \
+                    if (c < 0) { LK = c; } else { NK = c; EK = e; }                           \
+                }
 #define RS_SLOT(K, NK, EK, LK)                                                                \
             {                                                                                 \
                 const float lo[3] = {N.lo_x[K], N.lo_y[K], N.lo_z[K]};                        \
                 const float hi[3] = {N.hi_x[K], N.hi_y[K], N.hi_z[K]};                        \
                 float e;                                                                      \
                 const int c = N.child[K];                                                     \
-                if (c != INT32_MIN && slab32(lo, hi, rf, tmin32, best32, e)) {                \
-                    if (c < 0) { LK = c; } else { NK = c; EK = e; }                           \
-                }                                                                             \
+                RS_SLOT_BODY(c, NK, EK, LK)                                                   \
             }
             RS_SLOT(0, n0, e0, l0) RS_SLOT(1, n1, e1, l1) RS_SLOT(2, n2, e2, l2) RS_SLOT(3, n3, e3, l3)
 #undef RS_SLOT
+#undef RS_SLOT_BODY
+            const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
+                            (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
+            int next;
+            if (cnt == 0) {
+                next = -1;
+                if (sp > 0) { --sp; next = stk[sp * kBlock]; }
+            } else {
+                // sort descending by entry (farthest first, not-visited last): 5 compare-swaps
+#define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
+                RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
+#undef RS_CS
+                if (cnt > 1) { stk[sp * kBlock] = n0; ++sp; }
+                if (cnt > 2) { stk[sp * kBlock] = n1; ++sp; }
+                if (cnt > 3) { stk[sp * kBlock] = n2; ++sp; }
+                next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
+            }
+            // leaves of this node (their hits only shrink the range the next node is tested with)
             if (l0 != INT32_MIN) RS_LEAF(l0);
             if (l1 != INT32_MIN) RS_LEAF(l1);
             if (l2 != INT32_MIN) RS_LEAF(l2);
             if (l3 != INT32_MIN) RS_LEAF(l3);
-            const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
-                            (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
-            if (cnt == 0) {
-                if (sp == 0) break;
-                --sp;
-                node = stk[sp * kBlock];
-                continue;
-            }
-            // sort descending by entry (farthest first, not-visited last): 5 compare-swaps
-#define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
-            RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
-#undef RS_CS
-            if (cnt > 1) { stk[sp * kBlock] = n0; ++sp; }
-            if (cnt > 2) { stk[sp * kBlock] = n1; ++sp; }
-            if (cnt > 3) { stk[sp * kBlock] = n2; ++sp; }
-            node = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
+            if (next < 0) break;
+            node = next;
         }
     } else if (SO || !S.ref_order) {
         while (true) {

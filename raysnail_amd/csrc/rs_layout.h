@@ -119,6 +119,7 @@ struct DScene {
     const uint8_t* pclass;   // per prim handle: wavefront shading class of its material (spheres-only scenes)
     const DPrim* prims;
     const DSphere* spheres;
+    const DSphere* psph;     // spheres-only scenes: the sphere of prim handle p at psph[p] (no DPrim hop)
     const DRect* rects;
     const DBox* boxes;
     const DQuadric* quadrics;
