@@ -869,13 +869,19 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
             for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i) {
                 const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, pp.n_items - c0);
                 WS.counts = s->d_counts + chunk_i * (st->depth + 1) * cstride;
-                HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, s->d_rad, stream));
-                ++path_launches;
+                if (!sorted) {  // the sorted path generates camera rays inside its bounce-0 extend
+                    HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, s->d_rad, stream));
+                    ++path_launches;
+                }
                 const uint32_t wide = (uint32_t)(s->n_cu * 8);
                 for (uint32_t b = 0; sorted && b < st->depth; ++b) {
                     HIP_OK(hipEventRecord(kev[2 * ki], stream));
-                    HIP_OK(launch_wfs_extend(s->ds, WS, s->d_qptrs, b, cstride, pp.n_items, s->d_rad,
-                                             std::min(wide, (n + kBlock - 1) / kBlock), stream));
+                    if (b == 0)
+                        HIP_OK(launch_wfs_gen_extend(s->ds, dc, pp, WS, s->d_qptrs, cstride, c0, n, s->d_rad,
+                                                     std::min(wide, (n + kBlock - 1) / kBlock), stream));
+                    else
+                        HIP_OK(launch_wfs_extend(s->ds, WS, s->d_qptrs, b, cstride, pp.n_items, s->d_rad,
+                                                 std::min(wide, (n + kBlock - 1) / kBlock), stream));
                     HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
                     ++ki;
                     for (int k = 0; k < kWfsClasses; ++k)
@@ -929,28 +935,36 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
         stats->kernel_ms = kernel_ms;
         uint64_t seg = 0;
         for (int i = 0; i < 256; ++i) seg += cnt[i];
-        uint64_t cont = 0;
+        uint64_t cont = 0, seg0 = 0, cont0 = 0;
         if (!qc.empty()) {  // segments = sum over bounces of the extend queue lengths
             seg = 0;
             for (uint64_t c = 0; c < n_chunks_total; ++c)
                 for (uint32_t b = 0; b < st->depth; ++b) {
                     const uint32_t* q = &qc[(c * (st->depth + 1) + b) * cstride_f];
+                    uint64_t cb = 0;
+                    if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cb += q[1 + k];
+                    if (b == 0) { seg0 += q[0]; cont0 += cb; }
                     seg += q[0];
-                    if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cont += q[1 + k];
+                    cont += cb;
                 }
         }
         // algorithmic bytes of the dominant kernel (DESIGN.md Roofline):
         //  megakernel   : radiance out, 3 x f64 per sample
         //  wf extend    : ray in (2 x 32 B records) + hit out (16 B) per segment
-        //  wfs extend   : ray in (64 B) per segment; + hit (16 B) + queue slot (4 B) per shaded
-        //                 segment; + throughput/radiance records in (64 B), item (4 B) and radiance
-        //                 out (24 B) per path ending in extend (sky miss / light hit)
+        //  wfs extend   : bounces >= 1: ray in (64 B) per segment; + hit (16 B) + queue slot (4 B)
+        //                 per shaded segment; + throughput/radiance records in (64 B), item (4 B)
+        //                 and radiance out (24 B) per path ending in extend (sky miss / light hit).
+        //                 bounce 0 (fused with ray generation): radiance out (24 B) per sample that
+        //                 ends there (incl. masked); hit + queue slot + ray (64 B) + rng (16 B) +
+        //                 item (4 B) per shaded one
         if (!wavefront) {
             stats->kernel_id = RS_KERNEL_PATH_MEGA;
             stats->kernel_bytes = 24ull * (uint64_t)n_pix * N;
         } else if (cstride_f > 1) {
             stats->kernel_id = RS_KERNEL_WFS_EXTEND;
-            stats->kernel_bytes = 64ull * seg + 20ull * cont + 92ull * (seg - cont);
+            const uint64_t items = (uint64_t)n_pix * N, segr = seg - seg0, contr = cont - cont0;
+            stats->kernel_bytes = 24ull * (items - cont0) + 104ull * cont0 +
+                                  64ull * segr + 20ull * contr + 92ull * (segr - contr);
         } else {
             stats->kernel_id = RS_KERNEL_WF_EXTEND;
             stats->kernel_bytes = 80ull * seg;

@@ -60,6 +60,9 @@ hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, u
 // material-sorted variant (spheres-only scenes): counts stride per bounce = kWfsStride
 constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric, other
 constexpr uint32_t kWfsStride = 8;
+hipError_t launch_wfs_gen_extend(const DScene& s, const DCamera& c, const PathParams& p, const WfState& w,
+                                uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
+                                uint32_t blocks, hipStream_t st);
 hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);
 hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,

@@ -496,6 +496,15 @@ __device__ __forceinline__ void store_path(const WfSet& W, uint32_t p, const Ray
     W.rng[p] = make_uint4(rng.x, rng.y, rng.z, rng.w);
     W.item[p] = item;
 }
+// bounce-0 record of a fused gen+extend path: T = 1 and L = 0 are implied, not stored
+__device__ __forceinline__ void store_ray0(const WfSet& W, uint32_t p, const Ray& r, const Rng& rng, uint32_t item) {
+    D4 a, b;
+    a.x = r.o.x; a.y = r.o.y; a.z = r.o.z; a.w = r.time;
+    b.x = r.d.x; b.y = r.d.y; b.z = r.d.z; b.w = 0.0;
+    W.ray_o[p] = a; W.ray_d[p] = b;
+    W.rng[p] = make_uint4(rng.x, rng.y, rng.z, rng.w);
+    W.item[p] = item;
+}
 
 // wave-aggregated slot allocation: one atomic per wave, flagged lanes get consecutive slots
 __device__ __forceinline__ uint32_t wave_slot(bool flag, uint32_t* counter) {
@@ -543,6 +552,26 @@ __device__ __forceinline__ uint32_t block_slot1(bool flag, uint32_t* counter) {
 }
 
 // painter.rs:167-170 + camera.rs:77-85 for every (pixel, sample) item of a chunk
+// Camera sample `item` of the batch (painter.rs:154-187 jitter, camera.rs:77-85 ray): false for a
+// masked pixel (painter.rs:204-210) or depth 0 (camera.rs:161), whose radiance is 0.
+__device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
+    const uint32_t pl = (uint32_t)(item % P.n_pix_local);
+    const uint32_t sl = (uint32_t)(item / P.n_pix_local);
+    const uint32_t x = pl % P.width;
+    const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
+    const uint64_t pix = (uint64_t)y * P.width + x;
+    if ((P.mask && !P.mask[pix]) || P.depth == 0) return false;
+    const uint32_t s = P.s0 + sl;
+    rng.seed_from_u64(splitmix64(splitmix64(P.key_base ^ pix) ^ (uint64_t)s));
+    const uint32_t si = s % P.sqrt_spp, sj = s / P.sqrt_spp;
+    const double sq = (double)P.sqrt_spp;
+    const double xo = (double)x + ((double)si + rng.gen()) / sq;
+    const double yo = (double)y + ((double)sj + rng.gen()) / sq;
+    const double hh = (double)P.height;
+    r = camera_ray(C, xo / (double)P.width, (hh - 1.0 - yo) / hh, rng);
+    return true;
+}
+
 __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfState W, uint64_t item0, uint32_t n,
                                                    double* __restrict__ rad) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -552,24 +581,8 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
     uint64_t item = 0;
     if (i < n) {
         item = item0 + i;
-        const uint32_t pl = (uint32_t)(item % P.n_pix_local);
-        const uint32_t sl = (uint32_t)(item / P.n_pix_local);
-        const uint32_t x = pl % P.width;
-        const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
-        const uint64_t pix = (uint64_t)y * P.width + x;
-        if ((!P.mask || P.mask[pix]) && P.depth > 0) {
-            const uint32_t s = P.s0 + sl;
-            rng.seed_from_u64(splitmix64(splitmix64(P.key_base ^ pix) ^ (uint64_t)s));
-            const uint32_t si = s % P.sqrt_spp, sj = s / P.sqrt_spp;
-            const double sq = (double)P.sqrt_spp;
-            const double xo = (double)x + ((double)si + rng.gen()) / sq;
-            const double yo = (double)y + ((double)sj + rng.gen()) / sq;
-            const double hh = (double)P.height;
-            r = camera_ray(C, xo / (double)P.width, (hh - 1.0 - yo) / hh, rng);
-            live = true;
-        } else {
-            rad[item] = 0.0; rad[P.n_items + item] = 0.0; rad[2 * P.n_items + item] = 0.0;
-        }
+        live = camera_sample(C, P, item, r, rng);
+        if (!live) { rad[item] = 0.0; rad[P.n_items + item] = 0.0; rad[2 * P.n_items + item] = 0.0; }
     }
     const uint32_t slot = block_slot1(live, &W.counts[0]);
     if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), v3(0.0, 0.0, 0.0), rng, (uint32_t)item);
@@ -632,47 +645,72 @@ constexpr int kClsLight = 6;
 
 #ifndef RS_EXT_MIN_WAVES
 #define RS_EXT_MIN_WAVES 1  // 5 forces <=96 VGPRs but spills; measured slower (14.5 vs 13.8 ms)
+// (the fused bounce-0 variant asks for 4 waves: 128 VGPRs, no spill, instead of 132 at 3 waves)
 #endif
-__global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
+// GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
+// straight from registers, and only the paths that go on to shading are written (at index i, with
+// T = 1 and L = 0 implied for the bounce-0 shade kernels).
+template <bool GEN>
+__global__ __launch_bounds__(kBlock, GEN ? 4 : RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
-                                                      double* __restrict__ rad) {
+                                                      double* __restrict__ rad, DCamera C, PathParams P,
+                                                      uint64_t item0, uint32_t n_gen) {
     __shared__ int stk_all[kStackMax * kBlock];
     int* stk = stk_all + threadIdx.x;
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
-    const uint32_t n = cnt[0];
+    const uint32_t n = GEN ? n_gen : cnt[0];
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
         const uint32_t i = base + threadIdx.x;
         int cls = -1;
+        bool live = false;
         if (i < n) {
-            const Ray r = load_ray(cur, i);
-            double bend = RS_INF;
-            const int bp = traverse<true>(S, r, 0.0001, bend, stk);
-            V3 add;
-            bool done = true;
-            if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
-                add = background(S, r);
+            Ray r;
+            Rng rng;
+            uint32_t item = 0;
+            if (GEN) {
+                item = (uint32_t)(item0 + i);
+                live = camera_sample(C, P, item, r, rng);
+                if (!live) { rad[item] = 0.0; rad[n_items + item] = 0.0; rad[2 * n_items + item] = 0.0; }
             } else {
-                cls = (int)S.pclass[bp];
-                if (cls == kClsLight) {  // DiffuseLight: emitted, scatter None (camera.rs:172-176,250)
-                    const DPrim P = S.prims[bp];
-                    Hit h;
-                    sphere_hit(S.spheres[P.idx], P.mat, r, 0.0001, bend, h);
-                    add = emission(S.mats[P.mat >= 0 ? P.mat : S.default_mat], h.p);
-                    cls = -1;
+                r = load_ray(cur, i);
+                live = true;
+            }
+            if (live) {
+                double bend = RS_INF;
+                const int bp = traverse<true>(S, r, 0.0001, bend, stk);
+                V3 add;
+                bool done = true;
+                if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
+                    add = background(S, r);
                 } else {
-                    W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-                    done = false;
+                    cls = (int)S.pclass[bp];
+                    if (cls == kClsLight) {  // DiffuseLight: emitted, scatter None (camera.rs:172-176,250)
+                        const DPrim Pr = S.prims[bp];
+                        Hit h;
+                        sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
+                        add = emission(S.mats[Pr.mat >= 0 ? Pr.mat : S.default_mat], h.p);
+                        cls = -1;
+                    } else {
+                        W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+                        if (GEN) store_ray0(cur, i, r, rng, item);
+                        done = false;
+                    }
+                }
+                if (done) {
+                    D4 t4, l4;
+                    if (GEN) {
+                        t4.x = t4.y = t4.z = 1.0; l4.x = l4.y = l4.z = 0.0;
+                    } else {
+                        t4 = cur.thr[i]; l4 = cur.rad[i]; item = cur.item[i];
+                    }
+                    rad[item] = l4.x + t4.x * add.x;
+                    rad[n_items + item] = l4.y + t4.y * add.y;
+                    rad[2 * n_items + item] = l4.z + t4.z * add.z;
                 }
             }
-            if (done) {
-                const D4 t4 = cur.thr[i], l4 = cur.rad[i];
-                const uint32_t item = cur.item[i];
-                rad[item] = l4.x + t4.x * add.x;
-                rad[n_items + item] = l4.y + t4.y * add.y;
-                rad[2 * n_items + item] = l4.z + t4.z * add.z;
-            }
         }
+        if (GEN) block_slot1(live, &cnt[0]);  // segments at bounce 0 (stats)
         uint32_t* const cs[kClasses] = {&cnt[1], &cnt[2], &cnt[3], &cnt[4], &cnt[5]};
         const uint32_t slot = block_slot<kClasses>(cls, cs);
         if (cls >= 0) queues[cls][slot] = i;
@@ -702,9 +740,14 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
             finish_hit<true>(S, bp, r, 0.0001, hb.y, h);
-            const D4 t4 = cur.thr[i], l4 = cur.rad[i];
-            T = v3(t4.x, t4.y, t4.z);
-            L = v3(l4.x, l4.y, l4.z);
+            if (bounce == 0) {  // fused gen+extend: T = 1, L = 0 not stored
+                T = v3(1.0, 1.0, 1.0);
+                L = v3(0.0, 0.0, 0.0);
+            } else {
+                const D4 t4 = cur.thr[i], l4 = cur.rad[i];
+                T = v3(t4.x, t4.y, t4.z);
+                L = v3(l4.x, l4.y, l4.z);
+            }
             const uint4 g = cur.rng[i];
             rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
             item = cur.item[i];
@@ -824,7 +867,17 @@ hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, u
 
 hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st) {
-    hipLaunchKernelGGL(k_wfs_extend, dim3(blocks), dim3(kBlock), 0, st, s, w, queues, bounce, stride, n_items, rad);
+    hipLaunchKernelGGL(k_wfs_extend<false>, dim3(blocks), dim3(kBlock), 0, st, s, w, queues, bounce, stride, n_items, rad,
+                       DCamera{}, PathParams{}, 0ull, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_wfs_gen_extend(const DScene& s, const DCamera& c, const PathParams& p, const WfState& w,
+                                uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
+                                uint32_t blocks, hipStream_t st) {
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_wfs_extend<true>, dim3(blocks), dim3(kBlock), 0, st, s, w, queues, 0u, stride, p.n_items, rad,
+                       c, p, item0, n);
     return hipGetLastError();
 }
 
