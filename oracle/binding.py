@@ -66,12 +66,18 @@ def load() -> C.CDLL:
 
 
 class OracleScene:
-    """The same World replayed into the CPU restatement."""
+    """The same World replayed into the CPU restatement (or, with world=None, filled by
+    `fill(api, handle)` through a sink table -- e.g. the C++ SDL front end)."""
 
-    def __init__(self, world: World):
+    def __init__(self, world: World = None, fill=None):
         self.lib = load()
         self.h = C.c_void_p(self.lib.orc_scene_create())
-        realize(world, self.lib, self.h, "orc_")
+        if world is not None:
+            realize(world, self.lib, self.h, "orc_")
+        else:
+            from raysnail_amd.host_lib import sink_api_of
+            self.api = sink_api_of(self.lib, "orc_")
+            self.fill_result = fill(self.api, self.h)
         _check(self.lib, self.lib.orc_commit(self.h), "orc_")
 
     def __del__(self):

@@ -996,11 +996,19 @@ static double phong_highlight(const Vec3& dir_to_light, const Vec3& ray_dir, con
 }
 
 // camera.rs:156-255
+static int g_trace = 0;  // diagnostics: print each level of ray_color (orc_set_trace)
+
 static Vec3 ray_color(const Scene& sc, const Ray& ray, uint32_t depth, FastRng& rng, Counters& cnt) {
     if (depth == 0) return Vec3();
     HitRecord hit;
     cnt.segments++;
-    if (sc.world_hit(ray, 0.0001, INFINITY, hit)) {
+    const bool any = sc.world_hit(ray, 0.0001, INFINITY, hit);
+    if (g_trace)
+        std::fprintf(stderr, "depth %u o (%.17g %.17g %.17g) d (%.17g %.17g %.17g) hit %d t1 %.17g p (%.17g %.17g %.17g) n (%.17g %.17g %.17g) outside %d mat %d\n",
+                     depth, ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x, ray.direction.y, ray.direction.z,
+                     (int)any, hit.t1, hit.point.x, hit.point.y, hit.point.z, hit.normal.x, hit.normal.y, hit.normal.z,
+                     (int)hit.outside, hit.material ? hit.material->kind : -1);
+    if (any) {
         const Material* material = hit.material ? hit.material : &sc.default_material;
         Vec3 emitted;
         material->emitted(hit.u, hit.v, hit.point, emitted);
@@ -1029,6 +1037,7 @@ static Vec3 ray_color(const Scene& sc, const Ray& ray, uint32_t depth, FastRng& 
             if (pdf_val <= 0.0 || pdf_val != pdf_val) pdf_val = 1e-5;
             double spv = srec.pdf.value(scattered.direction);
             double mult = spv / pdf_val;
+            if (g_trace) std::fprintf(stderr, "   pdf_val %.17g spv %.17g mult %.17g light_multi %.17g\n", pdf_val, spv, mult, light_multi);
             Vec3 sample_color = light_multi * ray_color(sc, scattered, depth - 1, rng, cnt);
             Vec3 cfs = mul_color(sample_color, srec.color) * mult;
             return emitted + cfs;
@@ -1051,6 +1060,7 @@ static thread_local std::string g_err;
 static int fail(int code, const char* msg) { g_err = msg; return code; }
 
 const char* orc_last_error(void) { return g_err.c_str(); }
+void orc_set_trace(int on) { g_trace = on; }
 uint64_t orc_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
     return stream_key(seed, pass, pixel, sample);
 }

@@ -387,6 +387,13 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
     return true;
 }
 
+// A path that ends without an emission term (absorbed: scatter None; or the depth limit, where
+// ray_color returns 0) still multiplies that 0 through every level's factor in the reference's
+// recursion (camera.rs:241-247): (color * (light_multi * 0)) * mult. In the forward form that is
+// L + T * 0 -- which leaves L unchanged unless a factor was NaN / inf, where the recursion's
+// result is NaN and so is this one.
+__device__ __forceinline__ V3 close_path(V3 L, V3 T) { return L + T * 0.0; }
+
 // DiffuseLight emission (light.rs:33-35) of the hit's material, as a radiance vector
 __device__ __forceinline__ V3 emission(const DMaterial& M0, V3 p) {
     float c[3];
@@ -416,7 +423,9 @@ __device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray,
         const DMaterial& X = S.mats[ms];
         ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
     }
-    return shade_surface<-1, SO>(S, h, M0, S.mats[ms], ray, T, rng);
+    if (shade_surface<-1, SO>(S, h, M0, S.mats[ms], ray, T, rng)) return true;
+    L = close_path(L, T);  // scatter None
+    return false;
 }
 
 // ray_color iterated: one world.hit per level, at most `depth` levels. Returns the radiance.
@@ -428,9 +437,9 @@ __device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, int
         ++segs;
         Hit h;
         const bool ok = world_hit<SO>(S, ray, 0.0001, h, stk);
-        if (!shade_step<SO>(S, ok, h, ray, T, L, rng)) break;
+        if (!shade_step<SO>(S, ok, h, ray, T, L, rng)) return L;
     }
-    return L;
+    return close_path(L, T);  // depth limit: the next level would return 0
 }
 
 template <bool SO>
@@ -627,7 +636,11 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32
             const uint4 g = cur.rng[i];
             rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
             item = cur.item[i];
-            alive = shade_step<SO>(S, ok, h, r, T, L, rng) && (bounce + 1 < depth);
+            alive = shade_step<SO>(S, ok, h, r, T, L, rng);
+            if (alive && bounce + 1 >= depth) {  // depth limit
+                L = close_path(L, T);
+                alive = false;
+            }
             if (!alive) { rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z; }
         }
         const uint32_t slot = block_slot1(alive, &W.counts[bounce + 1]);
@@ -765,7 +778,10 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
                 cont = shade_surface<-1, true>(S, h, M0, S.mats[ms], r, T, rng);
             }
             alive = cont && (bounce + 1 < depth);
-            if (!alive) { rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z; }
+            if (!alive) {  // absorbed or depth limit: no emission term
+                L = close_path(L, T);
+                rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
+            }
         }
         const uint32_t slot = block_slot1(alive, &cnt_next[0]);
         if (alive) store_path(nxt, slot, r, T, L, rng, item);

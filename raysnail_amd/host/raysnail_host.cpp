@@ -1,0 +1,404 @@
+// libraysnail_host: the C++ host layer (include/raysnail.hpp) over the C-ABI of libraysnail_hip.
+// Object export, World / Camera / TakePhotoSettings, combine_pixels, and the C entry points.
+// The SDL front end lives in sdl_parser.cpp.
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "raysnail.hpp"
+
+namespace raysnail {
+
+namespace {
+thread_local std::string g_error;
+
+rs_texture_desc tex_desc(const Texture& t) {
+    rs_texture_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.kind = t.kind;
+    const float e[4] = {t.even.r, t.even.g, t.even.b, t.even.a};
+    const float o[4] = {t.odd.r, t.odd.g, t.odd.b, t.odd.a};
+    std::memcpy(d.even, e, sizeof(e));
+    std::memcpy(d.odd, o, sizeof(o));
+    d.scale = t.kind == RS_TEX_SOLID ? 1.0 : t.scale;
+    return d;
+}
+
+// rs_* take rs_scene*; the sink table is typed on void* so oracle tables fit the same slots.
+rs_scene* S(void* s) { return static_cast<rs_scene*>(s); }
+const rsh_sink_api kHipApi = {
+    [](void* s, const rs_material_desc* d, int32_t* id) { return rs_material(S(s), d, id); },
+    [](void* s, const double* c, double r, const double* v, int32_t m, uint32_t* h) { return rs_sphere(S(s), c, r, v, m, h); },
+    [](void* s, int32_t p, double k, double a0, double a1, double b0, double b1, int32_t m, uint32_t* h) {
+        return rs_aarect(S(s), p, k, a0, a1, b0, b1, m, h);
+    },
+    [](void* s, const double* p0, const double* p1, int32_t m, uint32_t* h) { return rs_box(S(s), p0, p1, m, h); },
+    [](void* s, const double* q, int32_t m, uint32_t* h) { return rs_quadric(S(s), q, m, h); },
+    [](void* s, const double* p, const double* n, uint32_t c, int32_t m, uint32_t* f) { return rs_triangles(S(s), p, n, c, m, f); },
+    [](void* s, uint32_t a, uint32_t b, int32_t m, uint32_t* h) { return rs_intersection(S(s), a, b, m, h); },
+    [](void* s, uint32_t a, uint32_t b, int32_t m, uint32_t* h) { return rs_difference(S(s), a, b, m, h); },
+    [](void* s, uint32_t o, const rs_transform* t, uint32_t n, uint32_t* h) { return rs_transformed(S(s), o, t, n, h); },
+    [](void* s, uint32_t h) { return rs_world_add(S(s), h); },
+    [](void* s, uint32_t h) { return rs_lights_add(S(s), h); },
+    [](void* s, const float* lo, const float* hi) { return rs_set_background(S(s), lo, hi); },
+    [](void* s, double t0, double t1) { return rs_set_time_range(S(s), t0, t1); },
+    []() { return rs_last_error(); },
+};
+
+void check_rs(int rc) {
+    if (rc != RS_OK) throw Error(rc, rs_last_error());
+}
+}  // namespace
+
+const rsh_sink_api& hip_sink_api() { return kHipApi; }
+
+void SceneSink::check(int rc) const {
+    if (rc != RS_OK) throw Error(rc, api.last_error ? api.last_error() : "scene sink error");
+}
+
+int32_t SceneSink::material(const MaterialRef& m) {
+    if (!m) return RS_NO_MATERIAL;
+    auto it = materials.find(m.get());
+    if (it != materials.end()) return it->second;
+    const int32_t id = m->export_to(*this);
+    materials.emplace(m.get(), id);
+    return id;
+}
+
+std::vector<uint32_t> SceneSink::object(const HittableRef& o) {
+    if (!o) throw Error(RS_E_INVALID, "null hittable");
+    auto it = objects.find(o.get());
+    if (it != objects.end()) return it->second;
+    std::vector<uint32_t> h = o->export_to(*this);
+    objects.emplace(o.get(), h);
+    return h;
+}
+
+// ---------------------------------------------------------------------------------- materials ----
+rs_material_desc Material::base_desc(int32_t kind, const Texture& t) const {
+    rs_material_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.kind = kind;
+    d.texture = tex_desc(t);
+    d.refractive = 1.0;
+    d.exponent = 0.0;
+    d.multiplier = 1.0;
+    d.mix_p = 0.5;
+    d.phong_factor = settings_.phong_factor;
+    d.phong_exponent = settings_.phong_exponent;
+    return d;
+}
+
+static int32_t add_material(SceneSink& sink, const rs_material_desc& d) {
+    int32_t id = -1;
+    sink.check(sink.api.material(sink.scene, &d, &id));
+    return id;
+}
+
+int32_t Lambertian::export_to(SceneSink& sink) const { return add_material(sink, base_desc(RS_MAT_LAMBERTIAN, tex_)); }
+int32_t Metal::export_to(SceneSink& sink) const { return add_material(sink, base_desc(RS_MAT_METAL, tex_)); }
+int32_t DiffuseMetal::export_to(SceneSink& sink) const {
+    rs_material_desc d = base_desc(RS_MAT_DIFFUSE_METAL, tex_);
+    d.exponent = exponent_;
+    return add_material(sink, d);
+}
+int32_t Dielectric::export_to(SceneSink& sink) const {
+    rs_material_desc d = base_desc(RS_MAT_DIELECTRIC, Texture::color(color_));
+    d.refractive = refractive_;
+    d.glass = glass_ ? 1 : 0;
+    return add_material(sink, d);
+}
+int32_t DiffuseLight::export_to(SceneSink& sink) const {
+    rs_material_desc d = base_desc(RS_MAT_DIFFUSE_LIGHT, tex_);
+    d.multiplier = mult_;
+    return add_material(sink, d);
+}
+int32_t MixedMaterial::export_to(SceneSink& sink) const {
+    const int32_t a = sink.material(m1_), b = sink.material(m2_);
+    rs_material_desc d = base_desc(RS_MAT_MIXED, Texture::color(Color{0.f, 0.f, 0.f, 1.f}));
+    d.mix_a = a;
+    d.mix_b = b;
+    d.mix_p = p_;
+    d.phong_factor = 0.0;   // unused: the library resolves the mix first and shades with the chosen
+    d.phong_exponent = 0;   // material's own settings
+    return add_material(sink, d);
+}
+
+// ----------------------------------------------------------------------------------- geometry ----
+AARectMetrics::AARectMetrics(double k_, std::pair<double, double> a_, std::pair<double, double> b_)
+    : k(k_), a(a_), b(b_) {
+    if (!(a.first < a.second) || !(b.first < b.second))  // rect.rs:27-28 assert!
+        throw Error(RS_E_INVALID, "AARectMetrics requires a0 < a1 and b0 < b1");
+}
+
+TriangleMesh::TriangleMesh(std::vector<double> positions, std::vector<double> normals, MaterialRef mat)
+    : pos_(std::move(positions)), nrm_(std::move(normals)), mat_(std::move(mat)) {
+    if (pos_.size() % 9 != 0 || (!nrm_.empty() && nrm_.size() != pos_.size()))
+        throw Error(RS_E_INVALID, "TriangleMesh: 9 doubles per triangle for positions (and normals)");
+}
+
+std::vector<uint32_t> Sphere::export_to(SceneSink& sink) const {
+    const double c[3] = {c_.x, c_.y, c_.z}, v[3] = {speed_.x, speed_.y, speed_.z};
+    uint32_t h = 0;
+    sink.check(sink.api.sphere(sink.scene, c, r_, v, sink.material(mat_), &h));
+    return {h};
+}
+
+std::vector<uint32_t> AARect::export_to(SceneSink& sink) const {
+    uint32_t h = 0;
+    sink.check(sink.api.aarect(sink.scene, plane_, m_.k, m_.a.first, m_.a.second, m_.b.first, m_.b.second,
+                               sink.material(mat_), &h));
+    return {h};
+}
+
+std::vector<uint32_t> Box::export_to(SceneSink& sink) const {
+    const double a[3] = {p0_.x, p0_.y, p0_.z}, b[3] = {p1_.x, p1_.y, p1_.z};
+    uint32_t h = 0;
+    sink.check(sink.api.box(sink.scene, a, b, sink.material(mat_), &h));
+    return {h};
+}
+
+std::vector<uint32_t> Quadric::export_to(SceneSink& sink) const {
+    uint32_t h = 0;
+    sink.check(sink.api.quadric(sink.scene, q_.data(), sink.material(mat_), &h));
+    return {h};
+}
+
+std::vector<uint32_t> TriangleMesh::export_to(SceneSink& sink) const {
+    const uint32_t n = (uint32_t)(pos_.size() / 9);
+    uint32_t first = 0;
+    sink.check(sink.api.triangles(sink.scene, pos_.data(), nrm_.empty() ? nullptr : nrm_.data(), n,
+                                  sink.material(mat_), &first));
+    std::vector<uint32_t> h(n);
+    for (uint32_t i = 0; i < n; ++i) h[i] = first + i;
+    return h;
+}
+
+static uint32_t single(const std::vector<uint32_t>& h, const char* what) {
+    if (h.size() != 1) throw Error(RS_E_UNSUPPORTED, std::string(what) + ": operand must be a single object");
+    return h[0];
+}
+
+std::vector<uint32_t> Intersection::export_to(SceneSink& sink) const {
+    const uint32_t a = single(sink.object(o1_), "Intersection"), b = single(sink.object(o2_), "Intersection");
+    uint32_t h = 0;
+    sink.check(sink.api.intersection(sink.scene, a, b, sink.material(mat_), &h));
+    return {h};
+}
+
+std::vector<uint32_t> Difference::export_to(SceneSink& sink) const {
+    const uint32_t a = single(sink.object(plus_), "Difference"), b = single(sink.object(minus_), "Difference");
+    uint32_t h = 0;
+    sink.check(sink.api.difference(sink.scene, a, b, sink.material(mat_), &h));
+    return {h};
+}
+
+std::vector<uint32_t> TfFacade::export_to(SceneSink& sink) const {
+    const std::vector<uint32_t> child = sink.object(obj_);
+    std::vector<uint32_t> out;
+    for (uint32_t c : child) {  // a transformed mesh is a transformed triangle each
+        uint32_t h = 0;
+        sink.check(sink.api.transformed(sink.scene, c, stack_.items().data(), (uint32_t)stack_.len(), &h));
+        out.push_back(h);
+    }
+    return out;
+}
+
+// -------------------------------------------------------------------------------------- World ----
+World::World(HittableList hittables, HittableList lights, Gradient background, std::pair<double, double> time_range)
+    : hittables_(std::move(hittables)), lights_(std::move(lights)), background_(background), time_range_(time_range) {}
+
+World::~World() {
+    if (scene_) rs_scene_destroy(scene_);
+}
+
+World::World(World&& o) noexcept
+    : hittables_(std::move(o.hittables_)), lights_(std::move(o.lights_)), background_(o.background_),
+      time_range_(o.time_range_), scene_(o.scene_) {
+    o.scene_ = nullptr;
+}
+
+World& World::operator=(World&& o) noexcept {
+    if (this != &o) {
+        if (scene_) rs_scene_destroy(scene_);
+        hittables_ = std::move(o.hittables_);
+        lights_ = std::move(o.lights_);
+        background_ = o.background_;
+        time_range_ = o.time_range_;
+        scene_ = o.scene_;
+        o.scene_ = nullptr;
+    }
+    return *this;
+}
+
+void World::export_to(SceneSink& sink) const {
+    const float lo[3] = {background_.lo.r, background_.lo.g, background_.lo.b};
+    const float hi[3] = {background_.hi.r, background_.hi.g, background_.hi.b};
+    sink.check(sink.api.set_background(sink.scene, lo, hi));
+    sink.check(sink.api.set_time_range(sink.scene, time_range_.first, time_range_.second));
+    for (const HittableRef& o : hittables_.objects())
+        for (uint32_t h : sink.object(o)) sink.check(sink.api.world_add(sink.scene, h));
+    for (const HittableRef& o : lights_.objects())
+        for (uint32_t h : sink.object(o)) sink.check(sink.api.lights_add(sink.scene, h));
+}
+
+rs_scene* World::device_scene() {
+    if (scene_) return scene_;
+    rs_scene* s = nullptr;
+    check_rs(rs_scene_create(&s));
+    try {
+        SceneSink sink(hip_sink_api(), s);
+        export_to(sink);
+        check_rs(rs_scene_commit(s));
+    } catch (...) {
+        rs_scene_destroy(s);
+        throw;
+    }
+    scene_ = s;
+    return scene_;
+}
+
+// ------------------------------------------------------------------------------------- Camera ----
+CameraBuilder::CameraBuilder() {
+    std::memset(&d_, 0, sizeof(d_));
+    d_.look_at[2] = -1.0;
+    d_.vup[1] = 1.0;
+    d_.fov = 90.0;
+    d_.aperture = 0.0;
+    d_.focus = 1.0;
+    d_.shutter = 0.0;
+    d_.width = 400;
+    d_.height = 200;
+}
+
+CameraBuilder& CameraBuilder::focus_to_look_at() {  // camera.rs: (look_at - look_from).length()
+    const double dx = d_.look_at[0] - d_.look_from[0], dy = d_.look_at[1] - d_.look_from[1],
+                 dz = d_.look_at[2] - d_.look_from[2];
+    d_.focus = std::sqrt(std::fma(dz, dz, std::fma(dx, dx, dy * dy)));  // length_squared, vec3.rs:152-160
+    return *this;
+}
+
+rs_render_settings TakePhotoSettings::settings() const {
+    rs_render_settings st;
+    std::memset(&st, 0, sizeof(st));
+    st.samples = samples_;
+    st.depth = depth_;
+    st.gamma = gamma_ ? 1 : 0;
+    st.mode = mode_;
+    st.seed = seed_;
+    st.pass = pass_;
+    st.row_begin = row_begin_;
+    st.row_end = row_end_;
+    st.row_step = row_step_;
+    return st;
+}
+
+std::vector<Pixel> TakePhotoSettings::shot_to_target(const char*, World& world, PainterTarget* target,
+                                                     PainterController*, const PixelController* pixel_map) {
+    const rs_camera_desc& cam = camera_.desc();
+    const size_t W = cam.width, H = cam.height;
+    std::vector<uint8_t> mask;
+    if (pixel_map) {
+        mask.resize(W * H);
+        for (size_t y = 0; y < H; ++y)
+            for (size_t x = 0; x < W; ++x) mask[y * W + x] = pixel_map->calculate_pixel(x, y) ? 1 : 0;
+    }
+    std::vector<Pixel> out(W * H, Pixel{0.f, 0.f, 0.f, 0.f});
+    const rs_render_settings st = settings();
+    check_rs(rs_render(world.device_scene(), &cam, &st, mask.empty() ? nullptr : mask.data(),
+                       reinterpret_cast<float*>(out.data()), &stats_));
+    if (target) {
+        for (size_t y = 0; y < H; ++y)
+            target->register_pixels(y, std::vector<Pixel>(out.begin() + y * W, out.begin() + (y + 1) * W));
+        target->register_pixels(H, {});  // end-of-pass sentinel (painter.rs:332)
+    }
+    return out;
+}
+
+void combine_pixels(std::vector<Pixel>& old_pixels, const std::vector<Pixel>& new_pixels, float p) {
+    if (old_pixels.size() != new_pixels.size()) throw Error(RS_E_INVALID, "combine_pixels: size mismatch");
+    for (size_t i = 0; i < new_pixels.size(); ++i) {
+        const Pixel& n = new_pixels[i];
+        if (n[0] == 0.f && n[1] == 0.f && n[2] == 0.f && n[3] == 0.f) continue;  // keep old
+        Pixel& o = old_pixels[i];
+        const float d = p + 1.0f;
+        for (int c = 0; c < 4; ++c) o[c] = (o[c] * p + n[c]) / d;
+    }
+}
+
+CliScene cli_scene(SceneData scene, size_t width, size_t height) {
+    if (!scene.camera) throw Error(RS_E_INVALID, "scene has no camera");  // scene_data.camera.unwrap()
+    const CameraData& cd = *scene.camera;
+    Camera camera = CameraBuilder()
+                        .look_from(cd.location)
+                        .look_at(cd.look_at)
+                        .fov(cd.fov_angle)
+                        .aperture(0.01)
+                        .focus(10.0)
+                        .width(width)
+                        .height(height)
+                        .build();
+    HittableList lights;
+    for (const LightData& l : scene.lights) {
+        auto mat = std::make_shared<DiffuseLight>(Texture::color(l.color));
+        mat->multiplier(1.7);
+        auto s1 = std::make_shared<Sphere>(l.location, 12.0, mat);
+        auto s2 = std::make_shared<Sphere>(*s1);  // rs.clone() into lights, rs into the world list
+        lights.add(s1);
+        scene.hittables.add(s2);
+    }
+    Gradient bg{Color{0.3f, 0.4f, 0.5f, 1.f}, Color{0.7f, 0.89f, 1.0f, 1.f}};
+    World world(std::move(scene.hittables), std::move(lights), bg, {0.0, camera.shutter_speed()});
+    return CliScene{camera, std::move(world)};
+}
+
+namespace detail {
+void set_error(const std::string& e) { g_error = e; }
+const char* last_error() { return g_error.c_str(); }
+}
+
+}  // namespace raysnail
+
+using namespace raysnail;
+
+template <class F>
+static int guarded(F&& f) {
+    try {
+        f();
+        detail::set_error("");
+        return RS_OK;
+    } catch (const Error& e) {
+        detail::set_error(e.what());
+        return e.code() ? e.code() : RS_E_INVALID;
+    } catch (const std::exception& e) {
+        detail::set_error(e.what());
+        return RS_E_INVALID;
+    }
+}
+
+extern "C" int rsh_sdl_build(const char* path, uint32_t width, uint32_t height, const rsh_sink_api* api, void* scene,
+                             rs_camera_desc* cam_out) {
+    return guarded([&] {
+        if (!path || !api || !scene) throw Error(RS_E_INVALID, "null argument");
+        CliScene sc = cli_scene(SdlParser::parse(path), width, height);
+        SceneSink sink(*api, scene);
+        sc.world.export_to(sink);
+        if (cam_out) *cam_out = sc.camera.desc();
+    });
+}
+
+extern "C" int rsh_sdl_render(const char* path, uint32_t width, uint32_t height, const rs_render_settings* st,
+                              float* out_rgba, rs_render_stats* stats) {
+    return guarded([&] {
+        if (!path || !st || !out_rgba) throw Error(RS_E_INVALID, "null argument");
+        CliScene sc = cli_scene(SdlParser::parse(path), width, height);
+        TakePhotoSettings photo = sc.camera.take_photo();
+        photo.samples(st->samples).depth(st->depth).gamma(st->gamma != 0).seed(st->seed).pass_index(st->pass)
+            .rows(st->row_begin, st->row_end, st->row_step).mode(st->mode);
+        std::vector<Pixel> px = photo.shot(nullptr, sc.world);
+        std::memcpy(out_rgba, px.data(), px.size() * sizeof(Pixel));
+        if (stats) *stats = photo.last_stats();
+    });
+}
+
+extern "C" const char* rsh_last_error(void) { return detail::last_error(); }

@@ -1,0 +1,87 @@
+"""ctypes binding of libraysnail_host.so, the C++ host layer (include/raysnail.hpp).
+
+The C++ layer holds the SDL front end (src/sdl_parser.rs restated) and the Rust-shaped object API;
+these two C entry points expose it to Python:
+
+* ``sdl_build(path, width, height, api, scene)`` -- parse an SDL file, apply the CLI's scene
+  conventions (src/bin/raysnail.rs:340-373) and replay the world into any scene sink (a table of
+  the rs_* scene-building functions: libraysnail_hip's own, or the CPU oracle's in the tests);
+  returns the camera.
+* ``sdl_render(path, width, height, settings)`` -- the same scene rendered on the GPU through the
+  C++ World / TakePhotoSettings path. Raises if the library is missing: there is no fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as A
+
+_LIB = None
+_F = C.CFUNCTYPE
+
+
+class rsh_sink_api(C.Structure):
+    """struct rsh_sink_api (include/raysnail.hpp): the scene-building half of the C-ABI as a table."""
+    _fields_ = [(name, C.c_void_p) for name in (
+        "material", "sphere", "aarect", "box", "quadric", "triangles", "intersection", "difference",
+        "transformed", "world_add", "lights_add", "set_background", "set_time_range", "last_error")]
+
+
+def sink_api_of(lib, prefix: str) -> rsh_sink_api:
+    """A sink table from a library exporting <prefix>material, <prefix>sphere, ... (rs_ or orc_)."""
+    api = rsh_sink_api()
+    for name, _ in rsh_sink_api._fields_:
+        setattr(api, name, C.cast(getattr(lib, prefix + name), C.c_void_p).value)
+    return api
+
+
+def lib_path() -> str:
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libraysnail_host.so")
+
+
+def load() -> C.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    A.load()  # libraysnail_hip first (the host library links it through $ORIGIN)
+    path = lib_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"libraysnail_host.so not built ({path}); run __graft_entry__.build()")
+    lib = C.CDLL(path)
+    lib.rsh_sdl_build.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(rsh_sink_api), C.c_void_p,
+                                  C.POINTER(A.rs_camera_desc)]
+    lib.rsh_sdl_build.restype = C.c_int
+    lib.rsh_sdl_render.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(A.rs_render_settings), C.c_void_p,
+                                   C.POINTER(A.rs_render_stats)]
+    lib.rsh_sdl_render.restype = C.c_int
+    lib.rsh_last_error.restype = C.c_char_p
+    _LIB = lib
+    return lib
+
+
+class HostError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise HostError(rc, load().rsh_last_error().decode())
+
+
+def sdl_build(path: str, width: int, height: int, api: rsh_sink_api, scene) -> A.rs_camera_desc:
+    cam = A.rs_camera_desc()
+    _check(load().rsh_sdl_build(os.fsencode(path), width, height, C.byref(api), scene, C.byref(cam)))
+    return cam
+
+
+def sdl_render(path: str, width: int, height: int, settings: A.rs_render_settings):
+    out = np.zeros((height, width, 4), dtype=np.float32)
+    stats = A.rs_render_stats()
+    _check(load().rsh_sdl_render(os.fsencode(path), width, height, C.byref(settings),
+                                 out.ctypes.data_as(C.c_void_p), C.byref(stats)))
+    return out, stats
