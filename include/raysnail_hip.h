@@ -215,6 +215,13 @@ int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
  * not computed on the GPU: 0). tmax must be +inf or the hit is dropped when t1 >= tmax. */
 int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin, double tmax, double* out);
 
+/* Radiance of samples s0 .. s0+n-1 of pixel (x, y) -- one ray_color (camera.rs:156-255) each, the
+ * camera sample and RNG stream exactly as rs_render draws them (st: samples, depth, seed, pass).
+ * out: n*4 doubles = [r, g, b, world.hit count], before the /N and gamma of into_color. Diagnostic
+ * (per-sample parity against the oracle); no reference counterpart. */
+int rs_probe_samples(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, uint32_t x, uint32_t y,
+                     uint32_t s0, uint32_t n, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,7 +16,9 @@ from raysnail_amd.api import World, realize, _check
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
-_LIB = None
+# the same restatement calling glibc's sin / cos / pow instead of include/rs_crmath.h
+GLIBC_LIB_PATH = os.path.join(HERE, "build", "liboracle_glibc.so")
+_LIBS = {}
 
 
 def build() -> str:
@@ -24,13 +26,12 @@ def build() -> str:
     return LIB_PATH
 
 
-def load() -> C.CDLL:
-    global _LIB
-    if _LIB is not None:
-        return _LIB
-    if not os.path.exists(LIB_PATH):
+def load(path: str = LIB_PATH) -> C.CDLL:
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
         build()
-    lib = C.CDLL(LIB_PATH)
+    lib = C.CDLL(path)
     for name, (res, args) in A.SCENE_SIGNATURES.items():
         f = getattr(lib, "orc_" + name)
         f.restype, f.argtypes = res, args
@@ -61,7 +62,8 @@ def load() -> C.CDLL:
     lib.orc_scatter.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_uint64,
                                 C.POINTER(C.c_double)]
     lib.orc_scatter.restype = C.c_int
-    _LIB = lib
+    lib.orc_set_trace.argtypes = [C.c_int]
+    _LIBS[path] = lib
     return lib
 
 
@@ -69,8 +71,8 @@ class OracleScene:
     """The same World replayed into the CPU restatement (or, with world=None, filled by
     `fill(api, handle)` through a sink table -- e.g. the C++ SDL front end)."""
 
-    def __init__(self, world: World = None, fill=None):
-        self.lib = load()
+    def __init__(self, world: World = None, fill=None, lib_path: str = LIB_PATH):
+        self.lib = load(lib_path)
         self.h = C.c_void_p(self.lib.orc_scene_create())
         if world is not None:
             realize(world, self.lib, self.h, "orc_")

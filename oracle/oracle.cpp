@@ -50,6 +50,7 @@
 // Build: oracle/Makefile (g++ -O2 -ffp-contract=off; FMA only where the reference calls mul_add).
 
 #include "../include/raysnail_hip.h"
+#include "../include/rs_crmath.h"
 
 #include <algorithm>
 #include <atomic>
@@ -198,21 +199,38 @@ static Vec3 random_unit_disk(FastRng& rng) {
     }
     return Vec3(0, 0, 0);
 }
+// libm semantics of the path: correctly rounded sin / cos / pow (include/rs_crmath.h, checked
+// against libquadmath by tests/test_crmath.py), shared with the GPU. Built with -DORC_GLIBC_MATH
+// this file calls glibc instead (liboracle_glibc.so), to measure what that choice changes.
+#ifdef ORC_GLIBC_MATH
+static inline void lm_sincos(double x, double* s, double* c) { *s = std::sin(x); *c = std::cos(x); }
+static inline double lm_pow(double x, double y) { return std::pow(x, y); }
+static inline bool lm_sin3_negative(double a, double b, double c) { return std::sin(a) * std::sin(b) * std::sin(c) < 0.0; }
+#else
+static inline void lm_sincos(double x, double* s, double* c) { rs_cr::sincos_cr(x, s, c); }
+static inline double lm_pow(double x, double y) { return rs_cr::pow_cr(x, y); }
+static inline bool lm_sin3_negative(double a, double b, double c) { return rs_cr::sin3_negative(a, b, c); }
+#endif
+
 // vec3.rs:100-111
 static Vec3 random_cosine_direction(FastRng& rng) {
     double r1 = rng.gen();
     double r2 = rng.gen();
     double q2 = std::sqrt(r2);
     double phi = 2.0 * PI * r1;
-    return Vec3(std::cos(phi) * q2, std::sin(phi) * q2, std::sqrt(1.0 - r2));
+    double sp, cp;
+    lm_sincos(phi, &sp, &cp);
+    return Vec3(cp * q2, sp * q2, std::sqrt(1.0 - r2));
 }
 // vec3.rs:115-126
 static Vec3 random_cosine_direction_exponent(double exponent, FastRng& rng) {
     double r1 = rng.gen();
-    double r2 = std::pow(rng.gen(), 1.0 / (exponent + 1.0));
+    double r2 = lm_pow(rng.gen(), 1.0 / (exponent + 1.0));
     double sin_theta = std::sqrt(1.0 - r2 * r2);
     double phi = 2.0 * PI * r1;
-    return Vec3(std::cos(phi) * sin_theta, std::sin(phi) * sin_theta, r2);
+    double sp, cp;
+    lm_sincos(phi, &sp, &cp);
+    return Vec3(cp * sin_theta, sp * sin_theta, r2);
 }
 
 // ---------------------------------------------------------------- ONB (onb.rs) ----
@@ -297,8 +315,7 @@ struct Texture {
     // checker.rs:21-30
     Color color(double, double, const Vec3& p) const {
         if (kind == RS_TEX_SOLID) return even;
-        double value = std::sin(scale * p.x) * std::sin(scale * p.y) * std::sin(scale * p.z);
-        return value < 0.0 ? odd : even;
+        return lm_sin3_negative(scale * p.x, scale * p.y, scale * p.z) ? odd : even;  // sin sin sin < 0
     }
 };
 

@@ -131,6 +131,9 @@ def load() -> C.CDLL:
     lib.rs_scene_create.argtypes = [C.POINTER(VP)]
     lib.rs_scene_destroy.argtypes = [VP]
     lib.rs_scene_commit.argtypes = [VP]
+    lib.rs_probe_samples.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), C.c_uint32,
+                                     C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
+    lib.rs_probe_samples.restype = C.c_int
     lib.rs_render.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), VP, VP,
                               C.POINTER(rs_render_stats)]
     lib.rs_render_device.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), VP, VP, VP,
@@ -150,5 +153,5 @@ EXPORTED_SYMBOLS = [
     "rs_abi_version", "rs_last_error", "rs_device_count", "rs_stream_key", "rs_scene_create", "rs_scene_destroy",
     "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
     "rs_difference", "rs_transformed", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
-    "rs_scene_commit", "rs_render", "rs_render_device", "rs_probe_world_hit",
+    "rs_scene_commit", "rs_render", "rs_render_device", "rs_probe_world_hit", "rs_probe_samples",
 ]

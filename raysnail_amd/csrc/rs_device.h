@@ -8,6 +8,7 @@
 //   AABB::hit slab test                              src/prelude/aabb.rs:20-38
 // The per-primitive / per-material functions cite their reference lines below.
 #pragma once
+#include "../../include/rs_crmath.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "rs_layout.h"
@@ -420,17 +421,17 @@ __device__ __forceinline__ V3 random_cosine_direction(Rng& rng) {
     double q2 = sqrt(r2);
     double phi = 2.0 * RS_PI * r1;
     double sp, cp;
-    sincos(phi, &sp, &cp);
+    rs_cr::sincos_cr(phi, &sp, &cp);  // correctly rounded (rs_crmath.h)
     return v3(cp * q2, sp * q2, sqrt(1.0 - r2));
 }
 // vec3.rs:115-126
 __device__ __forceinline__ V3 random_cosine_direction_exponent(double e, Rng& rng) {
     double r1 = rng.gen();
-    double r2 = pow(rng.gen(), 1.0 / (e + 1.0));
+    double r2 = rs_cr::pow_cr(rng.gen(), 1.0 / (e + 1.0));
     double st = sqrt(1.0 - r2 * r2);
     double phi = 2.0 * RS_PI * r1;
     double sp, cp;
-    sincos(phi, &sp, &cp);
+    rs_cr::sincos_cr(phi, &sp, &cp);
     return v3(cp * st, sp * st, r2);
 }
 
@@ -460,8 +461,7 @@ __device__ __forceinline__ V3 pdf_generate(const Pdf& p, Rng& rng) {
 __device__ __forceinline__ void tex_color(const DMaterial& m, V3 p, float c[3]) {
     bool odd = false;
     if (m.tex_kind == RS_TEX_CHECKER) {
-        double val = sin(m.tex_scale * p.x) * sin(m.tex_scale * p.y) * sin(m.tex_scale * p.z);
-        odd = val < 0.0;
+        odd = rs_cr::sin3_negative(m.tex_scale * p.x, m.tex_scale * p.y, m.tex_scale * p.z);
     }
     const float* s = odd ? m.odd : m.even;
     c[0] = s[0]; c[1] = s[1]; c[2] = s[2];

@@ -1181,6 +1181,28 @@ int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin,
     });
 }
 
+int rs_probe_samples(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, uint32_t x, uint32_t y,
+                     uint32_t s0, uint32_t n, double* out) {
+    return run([&] {
+        S(s);
+        if (!cam || !st || !out) throw Error(RS_E_INVALID, "null argument");
+        if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
+        if (x >= cam->width || y >= cam->height) throw Error(RS_E_INVALID, "pixel outside the frame");
+        const uint32_t sq = (uint32_t)std::floor(std::sqrt((double)st->samples));
+        if ((uint64_t)s0 + n > (uint64_t)sq * sq) throw Error(RS_E_INVALID, "sample index beyond floor(sqrt(samples))^2");
+        DeviceGuard g(s->device);
+        PathParams pp{};
+        pp.n_pix_local = cam->width * cam->height; pp.width = cam->width; pp.height = cam->height;
+        pp.row_begin = 0; pp.row_step = 1; pp.sqrt_spp = sq; pp.depth = st->depth;
+        pp.key_base = splitmix64_h(splitmix64_h(st->seed) ^ (uint64_t)st->pass);
+        double* dout = nullptr;
+        HIP_OK(hipMalloc((void**)&dout, (size_t)n * 4 * sizeof(double) + 8));
+        HIP_OK(launch_probe_sample(s->ds, make_camera(*cam), pp, s->spheres_only, x, y, s0, n, dout, nullptr));
+        HIP_OK(hipMemcpy(out, dout, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost));
+        (void)hipFree(dout);
+    });
+}
+
 int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask, float* out,
               rs_render_stats* stats) {
     return run([&] {

@@ -50,6 +50,8 @@ struct FinalParams {
 };
 
 // Megakernel: one thread per (pixel, sample) path; radiance -> rad[c * n_items + item].
+hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, bool so, uint32_t x, uint32_t y,
+                               uint32_t s0, uint32_t n, double* out, hipStream_t st);
 hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, bool spheres_only, double* rad,
                             unsigned long long* seg_counters, hipStream_t st);
 hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,

@@ -563,14 +563,9 @@ __device__ __forceinline__ uint32_t block_slot1(bool flag, uint32_t* counter) {
 // painter.rs:167-170 + camera.rs:77-85 for every (pixel, sample) item of a chunk
 // Camera sample `item` of the batch (painter.rs:154-187 jitter, camera.rs:77-85 ray): false for a
 // masked pixel (painter.rs:204-210) or depth 0 (camera.rs:161), whose radiance is 0.
-__device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
-    const uint32_t pl = (uint32_t)(item % P.n_pix_local);
-    const uint32_t sl = (uint32_t)(item / P.n_pix_local);
-    const uint32_t x = pl % P.width;
-    const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
+__device__ __forceinline__ void camera_sample_xy(const DCamera& C, const PathParams& P, uint32_t x, uint32_t y,
+                                                 uint32_t s, Ray& r, Rng& rng) {
     const uint64_t pix = (uint64_t)y * P.width + x;
-    if ((P.mask && !P.mask[pix]) || P.depth == 0) return false;
-    const uint32_t s = P.s0 + sl;
     rng.seed_from_u64(splitmix64(splitmix64(P.key_base ^ pix) ^ (uint64_t)s));
     const uint32_t si = s % P.sqrt_spp, sj = s / P.sqrt_spp;
     const double sq = (double)P.sqrt_spp;
@@ -578,6 +573,15 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
     const double yo = (double)y + ((double)sj + rng.gen()) / sq;
     const double hh = (double)P.height;
     r = camera_ray(C, xo / (double)P.width, (hh - 1.0 - yo) / hh, rng);
+}
+__device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
+    const uint32_t pl = (uint32_t)(item % P.n_pix_local);
+    const uint32_t sl = (uint32_t)(item / P.n_pix_local);
+    const uint32_t x = pl % P.width;
+    const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
+    const uint64_t pix = (uint64_t)y * P.width + x;
+    if ((P.mask && !P.mask[pix]) || P.depth == 0) return false;
+    camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
     return true;
 }
 
@@ -846,6 +850,32 @@ hipError_t launch_probe_hit(const DScene& s, const double* rays, uint32_t n, dou
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     if (!blocks) return hipSuccess;
     hipLaunchKernelGGL(k_probe_hit, dim3(blocks), dim3(kBlock), 0, st, s, rays, n, tmin, tmax, out);
+    return hipGetLastError();
+}
+
+// Diagnostic: the radiance and world.hit count of samples s0 .. s0+n-1 of pixel (x, y), each
+// through the megakernel's trace_path (tests/ per-sample parity; the oracle's orc_sample_radiance).
+template <bool SO>
+__global__ __launch_bounds__(kBlock) void k_probe_sample(DScene S, DCamera C, PathParams P, uint32_t x, uint32_t y,
+                                                        uint32_t s0, uint32_t n, double* __restrict__ out) {
+    __shared__ int stk_all[kStackMax * kBlock];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    Ray r;
+    Rng rng;
+    camera_sample_xy(C, P, x, y, s0 + i, r, rng);
+    uint32_t segs = 0;
+    const V3 L = trace_path<SO>(S, r, P.depth, rng, stk_all + threadIdx.x, segs);
+    out[4 * (size_t)i] = L.x; out[4 * (size_t)i + 1] = L.y; out[4 * (size_t)i + 2] = L.z;
+    out[4 * (size_t)i + 3] = (double)segs;
+}
+
+hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, bool so, uint32_t x, uint32_t y,
+                               uint32_t s0, uint32_t n, double* out, hipStream_t st) {
+    const uint32_t blocks = (n + kBlock - 1) / kBlock;
+    if (!blocks) return hipSuccess;
+    if (so) hipLaunchKernelGGL(k_probe_sample<true>, dim3(blocks), dim3(kBlock), 0, st, s, c, p, x, y, s0, n, out);
+    else hipLaunchKernelGGL(k_probe_sample<false>, dim3(blocks), dim3(kBlock), 0, st, s, c, p, x, y, s0, n, out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,87 @@
+"""Measure BASELINE.json's configs C2-C5 on one GPU (the bench line itself is C1-shaped, bench.py):
+one full frame each after a warm-up frame, plus the CPU oracle on a bounded row subset of the same
+frame (16 threads), scaled by samples. Writes one JSON object per config to stdout.
+
+usage: python tools/bench_configs.py [--only C3,C4] [--cpu-seconds 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def configs():
+    from raysnail_amd import scenes
+    return {
+        "C2": ("sdl/example.sdl + CLI lights, 800x500, 64 spp, depth 50",
+               lambda: scenes.example_sdl(800, 500), 64, 50),
+        "C3": ("RTIOW final scene (balls_scene seed 7 + light), 1920x1080, 256 spp, depth 50",
+               lambda: scenes.rtow_13_1(1920, 1080)[:2], 256, 50),
+        "C4": ("sdl/quadric.sdl + Cornell xz emitter, 1024x1024, 1024 spp, depth 50",
+               lambda: scenes.quadric_sdl(1024, 1024), 1024, 50),
+        "C5": ("synthetic 72k-triangle mesh + ground + light, 1920x1080, 512 -> 484 spp, depth 50",
+               lambda: scenes.mesh_scene(1920, 1080), 512, 50),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--mode", type=int, default=0)
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    from oracle.binding import OracleScene
+    only = set(filter(None, args.only.split(",")))
+    for key, (desc, build, spp, depth) in configs().items():
+        if only and key not in only:
+            continue
+        cam, world = build()
+        t0 = time.perf_counter()
+        ds = world.device_scene()
+        t_commit = time.perf_counter() - t0
+        H, W = cam.desc.height, cam.desc.width
+        # warm-up on a few rows (kernel load, workspace allocation)
+        cam.take_photo().samples(spp).depth(depth).seed(1).rows(0, 8, 1).mode(args.mode).shot(None, world)
+        photo = cam.take_photo().samples(spp).depth(depth).seed(1).mode(args.mode)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        img = photo.shot(None, world)
+        dt = time.perf_counter() - t0
+        st = photo.last_stats
+        gpu_msps = st.samples / dt / 1e6
+        # CPU oracle: rows 0::k with k chosen from a probe so the run takes ~cpu_seconds
+        orc = OracleScene(world)
+        probe_rows = max(1, H // 64)
+        ps = photo.rows(0, 0, H // probe_rows).settings()
+        t0 = time.perf_counter()
+        _, pst = orc.render(cam.desc, ps, threads=args.cpu_threads)
+        tp = time.perf_counter() - t0
+        per_sample = tp / max(1, pst.samples)
+        want = args.cpu_seconds / per_sample
+        k = max(1, int(round(st.samples / max(1.0, want))))
+        cs = photo.rows(0, 0, k).settings()
+        t0 = time.perf_counter()
+        ref, cst = orc.render(cam.desc, cs, threads=args.cpu_threads)
+        tc = time.perf_counter() - t0
+        cpu_msps = cst.samples / tc / 1e6
+        same_rows = bool((img[::k] == ref[::k]).all())
+        out = {"config": key, "workload": desc, "width": W, "height": H, "spp": int(spp ** 0.5) ** 2,
+               "depth": depth, "gpu": {"Msamples_per_s": round(gpu_msps, 2), "ms_per_frame": round(dt * 1e3, 2),
+                                       "kernel_ms": round(st.kernel_ms, 2), "segments": st.segments,
+                                       "segments_per_sample": round(st.segments / st.samples, 4),
+                                       "launches": st.launches, "commit_s": round(t_commit, 3)},
+               "cpu_baseline": {"Msamples_per_s": round(cpu_msps, 4), "threads": args.cpu_threads, "kind": "port",
+                                "sample": f"rows 0::{k} ({cst.samples} samples) in {tc:.1f} s"},
+               "speedup": round(gpu_msps / cpu_msps, 1), "sampled_rows_bit_identical": same_rows}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
