@@ -147,7 +147,7 @@ __device__ __forceinline__ bool rect_hit_raw(int ax0, int ax1, int ax2, double k
 
 // box.rs:125-149; faces in the order built by box.rs:55-105
 __device__ bool box_hit(const DBox& b, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h) {
-    Hit hs[2];
+    Hit h0, h1;  // the first two face hits in face order (two named records: no scratch array)
     int n = 0;
 #pragma unroll
     for (int f = 0; f < 6; ++f) {
@@ -155,14 +155,19 @@ __device__ bool box_hit(const DBox& b, int32_t mat, const Ray& r, double tmin, d
         if (f < 2)      { ax0 = 0; ax1 = 1; ax2 = 2; k = f == 0 ? b.mn[2] : b.mx[2]; a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[1]; b1 = b.mx[1]; }
         else if (f < 4) { ax0 = 1; ax1 = 2; ax2 = 0; k = f == 2 ? b.mn[0] : b.mx[0]; a0 = b.mn[1]; a1 = b.mx[1]; b0 = b.mn[2]; b1 = b.mx[2]; }
         else            { ax0 = 0; ax1 = 2; ax2 = 1; k = f == 4 ? b.mn[1] : b.mx[1]; a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[2]; b1 = b.mx[2]; }
-        Hit t;
-        if (n < 2 && rect_hit_raw(ax0, ax1, ax2, k, a0, a1, b0, b1, mat, r, tmin, tmax, t)) { hs[n] = t; ++n; }
+        if (n < 2) {
+            Hit t;
+            if (rect_hit_raw(ax0, ax1, ax2, k, a0, a1, b0, b1, mat, r, tmin, tmax, t)) {
+                if (n == 0) h0 = t; else h1 = t;
+                ++n;
+            }
+        }
     }
     if (n == 0) return false;
-    if (n == 1) { h = hs[0]; return true; }
+    if (n == 1) { h = h0; return true; }
     // with_normal (hit.rs:55-67): outside = true, normal as recorded by the face
-    if (hs[0].t1 < hs[1].t1) { h = hs[0]; h.t2 = hs[1].t1; }
-    else { h = hs[1]; h.t2 = hs[0].t1; }
+    if (h0.t1 < h1.t1) { h = h0; h.t2 = h1.t1; }
+    else { h = h1; h.t2 = h0.t1; }
     h.outside = 1;
     return true;
 }
@@ -217,6 +222,27 @@ __device__ __forceinline__ bool quadric_contains(const DQuadric& Q, V3 p) {  // 
 }
 
 // triangle_mesh.rs:85-131
+// tri_hit's accept test alone (the traversal's leaf test; the winner's record is recomputed)
+__device__ __forceinline__ bool tri_t(const DTri& T, const Ray& r, double tmin, double tmax, double& t_out) {
+    double g = r.d.x, hh = r.d.y, i = r.d.z;
+    double j = T.p0[0] - r.o.x, k = T.p0[1] - r.o.y, l = T.p0[2] - r.o.z;
+    double eihf = T.e * i - hh * T.f;
+    double gfdi = g * T.f - T.d * i;
+    double dheg = T.d * hh - T.e * g;
+    double denom = T.a * eihf + T.b * gfdi + T.c * dheg;
+    double beta = (j * eihf + k * gfdi + l * dheg) / denom;
+    if (beta < 0.0 || beta >= 1.0) return false;
+    double akjb = T.a * k - j * T.b;
+    double jcal = j * T.c - T.a * l;
+    double blkc = T.b * l - k * T.c;
+    double gamma = (i * akjb + hh * jcal + g * blkc) / denom;
+    if (gamma <= 0.0 || beta + gamma >= 1.0) return false;
+    double t = -(T.f * akjb + T.e * jcal + T.d * blkc) / denom;
+    if (!(t >= tmin && t <= tmax)) return false;
+    t_out = t;
+    return true;
+}
+
 __device__ bool tri_hit(const DTri& T, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h) {
     double g = r.d.x, hh = r.d.y, i = r.d.z;
     double j = T.p0[0] - r.o.x, k = T.p0[1] - r.o.y, l = T.p0[2] - r.o.z;
@@ -282,12 +308,11 @@ template <int L> struct Obj {
             bool ok1 = Obj<L - 1>::hit(S, C.a, r, tmin, tmax, h1);
             bool ok2 = Obj<L - 1>::hit(S, C.b, r, tmin, tmax, h2);
             if (!(ok1 && ok2)) return false;
-            bool first1 = h1.t1 < h2.t1;
-            const Hit& n0 = first1 ? h1 : h2;
-            const Hit& n1 = first1 ? h2 : h1;
-            int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
-            if (Obj<L - 1>::contains(S, o1, n0.p)) { h = n0; }
-            else if (Obj<L - 1>::contains(S, o0, n1.p)) { h = n1; }
+            const bool first1 = h1.t1 < h2.t1;
+            const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
+            const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
+            if (Obj<L - 1>::contains(S, o1, p0)) { h = first1 ? h1 : h2; }
+            else if (Obj<L - 1>::contains(S, o0, p1)) { h = first1 ? h2 : h1; }
             else return false;
             if (h.mat < 0) h.mat = P.mat;  // set_material_if_none (hit.rs:69-78)
             return true;

@@ -146,6 +146,7 @@ struct rs_scene {
     float bg_lo[3] = {0.3f, 0.4f, 0.5f}, bg_hi[3] = {0.7f, 0.89f, 1.0f};
     bool committed = false;
     bool spheres_only = false;
+    int scene_mode = kSmGeneric;        // rs_internal.h SceneMode
     bool ref_order = false;                 // BVH::hit recursion order needed (non-monotone objects)
     DScene ds{};
     std::vector<void*> dev;                 // scene allocations
@@ -596,6 +597,17 @@ void commit(rs_scene* s) {
         if (s->objs[h].kind != PK_SPHERE) s->spheres_only = false;
     }
     for (uint32_t h : s->lights) if (s->objs[h].kind != PK_SPHERE) s->spheres_only = false;
+    bool flat = true;  // only leaf kinds without nesting or order dependence
+    auto leaf_kind = [&](uint32_t h) {
+        const int k = s->objs[h].kind;
+        return k == PK_SPHERE || k == PK_RECT || k == PK_TRIANGLE;
+    };
+    for (uint32_t h : s->world) flat = flat && leaf_kind(h);
+    for (uint32_t h : s->lights) flat = flat && leaf_kind(h);
+    int nest = 0;
+    for (uint32_t h : s->world) nest = std::max(nest, s->nest_depth(h));
+    for (uint32_t h : s->lights) nest = std::max(nest, s->nest_depth(h));
+    s->scene_mode = s->spheres_only ? kSmSpheres : flat ? kSmFlat : nest == 0 ? kSmNest0 : nest <= 2 ? kSmNest2 : kSmGeneric;
     bool all_monotone = true;
     for (uint32_t h : s->world) all_monotone = all_monotone && s->monotone(h);
     s->ref_order = !all_monotone;
@@ -836,7 +848,7 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
             hipDeviceProp_t prop;
             HIP_OK(hipGetDeviceProperties(&prop, s->device));
             s->n_cu = prop.multiProcessorCount;
-            HIP_OK(wf_occupancy(s->spheres_only, &s->ext_bpc, &s->shade_bpc));
+            HIP_OK(wf_occupancy(s->scene_mode, &s->ext_bpc, &s->shade_bpc));
         }
     }
     const size_t n_kernel_ev = wavefront ? (size_t)n_chunks_total * st->depth : n_batches;
@@ -861,7 +873,7 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
         HIP_OK(hipEventRecord(ev[2 * bi], stream));
         if (!wavefront) {
             HIP_OK(hipEventRecord(kev[2 * ki], stream));
-            HIP_OK(launch_path_mega(s->ds, dc, pp, s->spheres_only, s->d_rad, s->d_cnt, stream));
+            HIP_OK(launch_path_mega(s->ds, dc, pp, s->scene_mode, s->d_rad, s->d_cnt, stream));
             HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
             ++ki;
             ++path_launches;
@@ -891,11 +903,11 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
                     HIP_OK(hipEventRecord(kev[2 * ki], stream));
-                    HIP_OK(launch_wf_extend(s->ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock), s->spheres_only, stream));
+                    HIP_OK(launch_wf_extend(s->ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
                     ++ki;
                     HIP_OK(launch_wf_shade(s->ds, WS, b, st->depth, pp.n_items, s->d_rad,
-                                           std::min(shade_blocks, (n + kBlock - 1) / kBlock), s->spheres_only, stream));
+                                           std::min(shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     path_launches += 2;
                 }
             }
@@ -1197,7 +1209,7 @@ int rs_probe_samples(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
         pp.key_base = splitmix64_h(splitmix64_h(st->seed) ^ (uint64_t)st->pass);
         double* dout = nullptr;
         HIP_OK(hipMalloc((void**)&dout, (size_t)n * 4 * sizeof(double) + 8));
-        HIP_OK(launch_probe_sample(s->ds, make_camera(*cam), pp, s->spheres_only, x, y, s0, n, dout, nullptr));
+        HIP_OK(launch_probe_sample(s->ds, make_camera(*cam), pp, s->scene_mode, x, y, s0, n, dout, nullptr));
         HIP_OK(hipMemcpy(out, dout, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(dout);
     });

@@ -10,6 +10,15 @@ constexpr int kBlock = 256;      // 4 waves of 64
 constexpr int kStackMax = 24;    // per-thread BVH stack entries (LDS, 24 KiB/block -> 6 blocks/CU); host enforces tree depth
 
 // One batch of camera samples: items = n_pix_local * n_samp_batch, item -> (sample, pixel).
+// Scene modes (a template parameter of every path kernel): kSmSpheres -- world and lights are
+// spheres only (prim-indexed sphere copy, material-sorted wavefront); kSmFlat -- spheres, rects and
+// triangles only (no CSG / transforms / boxes / quadrics: leaf tests without the nested object
+// machinery); kSmNest0 / kSmNest2 -- anything with at most 0 / 2 levels of CSG / TfFacade nesting
+// (the nested-object code is instantiated only as deep as the scene needs: fewer registers, no
+// scratch); kSmGeneric -- up to RS_MAX_NEST levels.
+enum SceneMode { kSmGeneric = 0, kSmSpheres = 1, kSmFlat = 2, kSmNest0 = 3, kSmNest2 = 4 };
+constexpr int nest_of(int sm) { return sm == kSmNest0 ? 0 : sm == kSmNest2 ? 2 : sm == kSmGeneric ? RS_MAX_NEST : 0; }
+
 struct PathParams {
     uint64_t n_items;
     uint32_t n_pix_local;   // pixels on the row lattice
@@ -50,15 +59,15 @@ struct FinalParams {
 };
 
 // Megakernel: one thread per (pixel, sample) path; radiance -> rad[c * n_items + item].
-hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, bool so, uint32_t x, uint32_t y,
+hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
                                uint32_t s0, uint32_t n, double* out, hipStream_t st);
-hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, bool spheres_only, double* rad,
+hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, int sm, double* rad,
                             unsigned long long* seg_counters, hipStream_t st);
 hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
                          hipStream_t st);
-hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, bool so, hipStream_t st);
+hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
-                           uint32_t blocks, bool so, hipStream_t st);
+                           uint32_t blocks, int sm, hipStream_t st);
 // material-sorted variant (spheres-only scenes): counts stride per bounce = kWfsStride
 constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric, other
 constexpr uint32_t kWfsStride = 8;
@@ -70,7 +79,7 @@ hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const*
 hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
-hipError_t wf_occupancy(bool so, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
+hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
 hipError_t launch_probe_hit(const DScene& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
                             hipStream_t st);
 // acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic).

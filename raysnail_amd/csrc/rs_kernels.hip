@@ -11,6 +11,18 @@
 #include "rs_device.h"
 #include "rs_internal.h"
 
+// instantiate a launch for the scene mode (rs_internal.h SceneMode) as the constant SMC
+#define RS_SM_DISPATCH(sm, ...)                                            \
+    do {                                                                   \
+        switch (sm) {                                                      \
+        case kSmSpheres: { constexpr int SMC = kSmSpheres; __VA_ARGS__; break; } \
+        case kSmFlat: { constexpr int SMC = kSmFlat; __VA_ARGS__; break; }       \
+        case kSmNest0: { constexpr int SMC = kSmNest0; __VA_ARGS__; break; }     \
+        case kSmNest2: { constexpr int SMC = kSmNest2; __VA_ARGS__; break; }     \
+        default: { constexpr int SMC = kSmGeneric; __VA_ARGS__; break; }         \
+        }                                                                  \
+    } while (0)
+
 namespace rs {
 
 // aabb.rs:20-38 with inv = 1/d[i] precomputed per ray (the reference recomputes the same value
@@ -115,25 +127,53 @@ __device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere&
     bend = best; best = t; bp = p;
 }
 
+// Nested-object entry points: Obj<L> instantiated only as deep as the scene mode needs.
+template <int SM>
+__device__ __forceinline__ bool obj_hit(const DScene& S, int p, const Ray& r, double tmin, double tmax, Hit& h) {
+    return Obj<nest_of(SM)>::hit(S, p, r, tmin, tmax, h);
+}
+template <int SM>
+__device__ __forceinline__ V3 obj_random(const DScene& S, int p, V3 origin, Rng& rng) {
+    return Obj<nest_of(SM)>::random(S, p, origin, rng);
+}
+
+// Object hit for flat scenes (spheres, rects, triangles; no nesting): Obj<L>::hit's leaf cases only.
+__device__ __forceinline__ bool flat_hit(const DScene& S, const DPrim& P, const Ray& r, double tmin, double tmax, Hit& h) {
+    if (P.kind == PK_TRIANGLE) return tri_hit(S.tris[P.idx], P.mat, r, tmin, tmax, h);
+    if (P.kind == PK_RECT) {
+        const DRect& R = S.rects[P.idx];
+        return rect_hit_raw(R.ax0, R.ax1, R.ax2, R.k, R.a0, R.a1, R.b0, R.b1, P.mat, r, tmin, tmax, h);
+    }
+    return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, tmax, h);
+}
+
 // Leaf: the object is accepted iff its exact own bbox passes (aabb.rs:20-38, BVH leaf box) AND it
 // hits within [tmin, best). Both are pure, so the cheap test runs first: for spheres the
 // discriminant, and the exact box only for spheres that hit.
-template <bool SO>
+template <int SM>
 __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, double tmin, double& best, double& bend,
                                           int& bp) {
-    if (SO) {  // prim-indexed sphere copy: one dependent load fewer than prims[p] -> spheres[idx]
+    if (SM == kSmSpheres) {  // prim-indexed sphere copy: one dependent load fewer than prims[p] -> spheres[idx]
         test_sphere_leaf(S, S.psph[p], p, r, tmin, best, bend, bp);
         return;
     }
     const DPrim P = S.prims[p];
     if (P.kind == PK_SPHERE) {
         test_sphere_leaf(S, S.spheres[P.idx], p, r, tmin, best, bend, bp);
+    } else if (SM == kSmFlat && P.kind == PK_TRIANGLE) {  // triangle first (most leaves fail its beta test)
+        double t;
+        if (!tri_t(S.tris[P.idx], r, tmin, best, t)) return;
+        const DBox64& B = S.pbox[p];
+        const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+        if (!slab64(B.lo, B.hi, r.o, inv, tmin, best)) return;
+        bend = best; best = t; bp = p;
     } else {
         const DBox64& B = S.pbox[p];
         const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
         if (!slab64(B.lo, B.hi, r.o, inv, tmin, best)) return;
         Hit tmp;
-        if (Obj<RS_MAX_NEST>::hit(S, p, r, tmin, best, tmp)) { bend = best; best = tmp.t1; bp = p; }
+        const bool ok = SM == kSmFlat ? flat_hit(S, P, r, tmin, best, tmp) : obj_hit<SM>(S, p, r, tmin, best, tmp);
+        if (ok) { bend = best; best = tmp.t1; bp = p; }
     }
 }
 
@@ -146,7 +186,7 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, 
 //    Each child box is tested when the recursion would visit it (the deferred right child is
 //    re-read from its parent when popped), so the tests see the same range as BVH::hit.
 // stk: this thread's column of the block's LDS stack (stride kBlock).
-template <bool SO>
+template <int SM>
 __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, int* stk) {
     if (S.root < 0) return -1;
     const RayF rf = make_rayf(r.o, v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z));
@@ -159,7 +199,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
 #define RS_LEAF(code)                                                          \
     do {                                                                       \
         const int bp_prev = bp;                                                \
-        test_leaf<SO>(S, ~(code), r, tmin, best, bend, bp);                    \
+        test_leaf<SM>(S, ~(code), r, tmin, best, bend, bp);                    \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
     if (S.root4 >= 0) {
@@ -212,7 +252,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
             if (next < 0) break;
             node = next;
         }
-    } else if (SO || !S.ref_order) {
+    } else if ((SM == kSmSpheres) || !S.ref_order) {
         while (true) {
             const DNode N = S.nodes[node];
             float e0, e1;
@@ -277,21 +317,22 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
 }
 
 // Recompute the full record of the winner with the exact range it was accepted under.
-template <bool SO>
+template <int SM>
 __device__ __forceinline__ bool finish_hit(const DScene& S, int bp, const Ray& r, double tmin, double bend, Hit& h) {
     if (bp < 0) return false;
-    if (SO || S.prims[bp].kind == PK_SPHERE) {
+    if ((SM == kSmSpheres) || S.prims[bp].kind == PK_SPHERE) {
         const DPrim P = S.prims[bp];
         return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, bend, h);
     }
-    return Obj<RS_MAX_NEST>::hit(S, bp, r, tmin, bend, h);
+    if (SM == kSmFlat) return flat_hit(S, S.prims[bp], r, tmin, bend, h);
+    return obj_hit<SM>(S, bp, r, tmin, bend, h);
 }
 
-template <bool SO>
+template <int SM>
 __device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, int* stk) {
     double bend;
-    const int bp = traverse<SO>(S, r, tmin, bend, stk);
-    return finish_hit<SO>(S, bp, r, tmin, bend, h);
+    const int bp = traverse<SM>(S, r, tmin, bend, stk);
+    return finish_hit<SM>(S, bp, r, tmin, bend, h);
 }
 
 // camera.rs:94-100
@@ -305,7 +346,7 @@ __device__ __forceinline__ double phong_highlight(V3 dir_to_light, V3 ray_dir, V
 // of camera.rs:176-247. KIND is the material class when known at compile time (material-sorted
 // wavefront shading) or -1 for a runtime switch. M0 = the hit's material (settings() source),
 // M = the material that scatters. Returns true when the path continues.
-template <int KIND, bool SO>
+template <int KIND, int SM>
 __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, const DMaterial& M0, const DMaterial& M,
                                               Ray& ray, V3& T, Rng& rng) {
     const int kind = KIND >= 0 ? KIND : M.kind;
@@ -367,8 +408,9 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
         pdf_val = 0.3183098861837907;
         const uint32_t li = rng.next_u32() % (uint32_t)S.n_lights;  // list.rs:49-52
         V3 rv;
-        if (SO) rv = Obj<0>::sphere_random(S.spheres[S.prims[S.lights[li]].idx], h.p, rng);
-        else rv = Obj<RS_MAX_NEST>::random(S, S.lights[li], h.p, rng);
+        if (SM == kSmSpheres) rv = Obj<0>::sphere_random(S.spheres[S.prims[S.lights[li]].idx], h.p, rng);
+        else if (SM == kSmFlat) rv = Obj<0>::random(S, S.lights[li], h.p, rng);  // no nesting below a leaf
+        else rv = obj_random<SM>(S, S.lights[li], h.p, rng);
         V3 dl = unit(rv);
         if (M0.phong_factor > 0.0) light_multi += phong_highlight(-dl, ray.d, h.n, M0.phong_exponent, M0.phong_factor);
         nr.o = ray_at(ray, h.t1 - 0.0002);
@@ -404,7 +446,7 @@ __device__ __forceinline__ V3 emission(const DMaterial& M0, V3 p) {
 // One level of TakePhotoSettings::ray_color (camera.rs:156-255) after world.hit: adds this
 // level's contribution to L and, when the recursion continues, replaces `ray` and multiplies the
 // path throughput T by this level's factor. Returns true when the path continues.
-template <bool SO>
+template <int SM>
 __device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray, V3& T, V3& L, Rng& rng) {
     if (!hit_ok) {  // camera.rs:253-254 background
         V3 bg = background(S, ray);
@@ -423,26 +465,26 @@ __device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray,
         const DMaterial& X = S.mats[ms];
         ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
     }
-    if (shade_surface<-1, SO>(S, h, M0, S.mats[ms], ray, T, rng)) return true;
+    if (shade_surface<-1, SM>(S, h, M0, S.mats[ms], ray, T, rng)) return true;
     L = close_path(L, T);  // scatter None
     return false;
 }
 
 // ray_color iterated: one world.hit per level, at most `depth` levels. Returns the radiance.
-template <bool SO>
+template <int SM>
 __device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, int* stk, uint32_t& segs) {
     V3 T = v3(1.0, 1.0, 1.0);
     V3 L = v3(0.0, 0.0, 0.0);
     for (uint32_t d = depth; d > 0; --d) {
         ++segs;
         Hit h;
-        const bool ok = world_hit<SO>(S, ray, 0.0001, h, stk);
-        if (!shade_step<SO>(S, ok, h, ray, T, L, rng)) return L;
+        const bool ok = world_hit<SM>(S, ray, 0.0001, h, stk);
+        if (!shade_step<SM>(S, ok, h, ray, T, L, rng)) return L;
     }
     return close_path(L, T);  // depth limit: the next level would return 0
 }
 
-template <bool SO>
+template <int SM>
 __global__ __launch_bounds__(kBlock) void k_path_mega(DScene S, DCamera C, PathParams P, double* __restrict__ rad,
                                                       unsigned long long* __restrict__ seg_counters) {
     __shared__ int stk_all[kStackMax * kBlock];
@@ -469,7 +511,7 @@ __global__ __launch_bounds__(kBlock) void k_path_mega(DScene S, DCamera C, PathP
             const double u = xo / (double)P.width;
             const double v = (hh - 1.0 - yo) / hh;
             Ray r = camera_ray(C, u, v, rng);
-            L = trace_path<SO>(S, r, P.depth, rng, stk, segs);
+            L = trace_path<SM>(S, r, P.depth, rng, stk, segs);
         }
         rad[item] = L.x;
         rad[P.n_items + item] = L.y;
@@ -601,7 +643,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
     if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), v3(0.0, 0.0, 0.0), rng, (uint32_t)item);
 }
 
-template <bool SO>
+template <int SM>
 __global__ __launch_bounds__(kBlock) void k_wf_extend(DScene S, WfState W, uint32_t bounce) {
     __shared__ int stk_all[kStackMax * kBlock];
     int* stk = stk_all + threadIdx.x;
@@ -610,12 +652,12 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DScene S, WfState W, uint3
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const Ray r = load_ray(cur, i);
         double bend = RS_INF;
-        const int bp = traverse<SO>(S, r, 0.0001, bend, stk);
+        const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
     }
 }
 
-template <bool SO>
+template <int SM>
 __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32_t bounce, uint32_t depth,
                                                     uint64_t n_items, double* __restrict__ rad) {
     const uint32_t n = W.counts[bounce];
@@ -633,14 +675,14 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
-            const bool ok = finish_hit<SO>(S, bp, r, 0.0001, hb.y, h);
+            const bool ok = finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
             const D4 t4 = cur.thr[i], l4 = cur.rad[i];
             T = v3(t4.x, t4.y, t4.z);
             L = v3(l4.x, l4.y, l4.z);
             const uint4 g = cur.rng[i];
             rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
             item = cur.item[i];
-            alive = shade_step<SO>(S, ok, h, r, T, L, rng);
+            alive = shade_step<SM>(S, ok, h, r, T, L, rng);
             if (alive && bounce + 1 >= depth) {  // depth limit
                 L = close_path(L, T);
                 alive = false;
@@ -695,7 +737,7 @@ __global__ __launch_bounds__(kBlock, GEN ? 4 : RS_EXT_MIN_WAVES) void k_wfs_exte
             }
             if (live) {
                 double bend = RS_INF;
-                const int bp = traverse<true>(S, r, 0.0001, bend, stk);
+                const int bp = traverse<kSmSpheres>(S, r, 0.0001, bend, stk);
                 V3 add;
                 bool done = true;
                 if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
@@ -756,7 +798,7 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
-            finish_hit<true>(S, bp, r, 0.0001, hb.y, h);
+            finish_hit<kSmSpheres>(S, bp, r, 0.0001, hb.y, h);
             if (bounce == 0) {  // fused gen+extend: T = 1, L = 0 not stored
                 T = v3(1.0, 1.0, 1.0);
                 L = v3(0.0, 0.0, 0.0);
@@ -838,7 +880,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __
     for (int k = 0; k < 13; ++k) o[k] = 0.0;
     // range end handled by clamping best: world_hit starts from +inf, so emulate [tmin, tmax) by a
     // post-check only when tmax is infinite (the render path always passes +inf)
-    if (world_hit<false>(S, r, tmin, h, stk_all + threadIdx.x) && h.t1 < tmax) {
+    if (world_hit<kSmGeneric>(S, r, tmin, h, stk_all + threadIdx.x) && h.t1 < tmax) {
         o[0] = 1.0; o[1] = h.t1; o[2] = h.t2;
         o[3] = h.p.x; o[4] = h.p.y; o[5] = h.p.z; o[6] = h.n.x; o[7] = h.n.y; o[8] = h.n.z;
         o[11] = h.outside ? 1.0 : 0.0; o[12] = (double)h.mat;
@@ -855,7 +897,7 @@ hipError_t launch_probe_hit(const DScene& s, const double* rays, uint32_t n, dou
 
 // Diagnostic: the radiance and world.hit count of samples s0 .. s0+n-1 of pixel (x, y), each
 // through the megakernel's trace_path (tests/ per-sample parity; the oracle's orc_sample_radiance).
-template <bool SO>
+template <int SM>
 __global__ __launch_bounds__(kBlock) void k_probe_sample(DScene S, DCamera C, PathParams P, uint32_t x, uint32_t y,
                                                         uint32_t s0, uint32_t n, double* __restrict__ out) {
     __shared__ int stk_all[kStackMax * kBlock];
@@ -865,28 +907,25 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(DScene S, DCamera C, Pa
     Rng rng;
     camera_sample_xy(C, P, x, y, s0 + i, r, rng);
     uint32_t segs = 0;
-    const V3 L = trace_path<SO>(S, r, P.depth, rng, stk_all + threadIdx.x, segs);
+    const V3 L = trace_path<SM>(S, r, P.depth, rng, stk_all + threadIdx.x, segs);
     out[4 * (size_t)i] = L.x; out[4 * (size_t)i + 1] = L.y; out[4 * (size_t)i + 2] = L.z;
     out[4 * (size_t)i + 3] = (double)segs;
 }
 
-hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, bool so, uint32_t x, uint32_t y,
+hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
                                uint32_t s0, uint32_t n, double* out, hipStream_t st) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     if (!blocks) return hipSuccess;
-    if (so) hipLaunchKernelGGL(k_probe_sample<true>, dim3(blocks), dim3(kBlock), 0, st, s, c, p, x, y, s0, n, out);
-    else hipLaunchKernelGGL(k_probe_sample<false>, dim3(blocks), dim3(kBlock), 0, st, s, c, p, x, y, s0, n, out);
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_probe_sample<SMC>, dim3(blocks), dim3(kBlock), 0, st, s, c, p, x, y, s0, n, out));
     return hipGetLastError();
 }
 
-hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, bool spheres_only, double* rad,
+hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, int sm, double* rad,
                             unsigned long long* seg_counters, hipStream_t st) {
     const uint64_t blocks = (p.n_items + kBlock - 1) / kBlock;
     if (blocks == 0) return hipSuccess;
-    if (spheres_only)
-        hipLaunchKernelGGL(k_path_mega<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s, c, p, rad, seg_counters);
-    else
-        hipLaunchKernelGGL(k_path_mega<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s, c, p, rad, seg_counters);
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_path_mega<SMC>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s, c, p, rad,
+                                          seg_counters));
     return hipGetLastError();
 }
 
@@ -898,16 +937,14 @@ hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w
     return hipGetLastError();
 }
 
-hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, bool so, hipStream_t st) {
-    if (so) hipLaunchKernelGGL(k_wf_extend<true>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce);
-    else hipLaunchKernelGGL(k_wf_extend<false>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce);
+hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st) {
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce));
     return hipGetLastError();
 }
 
 hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
-                           uint32_t blocks, bool so, hipStream_t st) {
-    if (so) hipLaunchKernelGGL(k_wf_shade<true>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce, depth, n_items, rad);
-    else hipLaunchKernelGGL(k_wf_shade<false>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce, depth, n_items, rad);
+                           uint32_t blocks, int sm, hipStream_t st) {
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_shade<SMC>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce, depth, n_items, rad));
     return hipGetLastError();
 }
 
@@ -939,15 +976,13 @@ hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* q
     return hipGetLastError();
 }
 
-hipError_t wf_occupancy(bool so, int* e, int* sh) {
-    hipError_t r;
-    if (so) {
-        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<true>), kBlock, 0);
-        if (r == hipSuccess) r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<true>), kBlock, 0);
-    } else {
-        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<false>), kBlock, 0);
-        if (r == hipSuccess) r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<false>), kBlock, 0);
-    }
+hipError_t wf_occupancy(int sm, int* e, int* sh) {
+    hipError_t r = hipSuccess;
+    RS_SM_DISPATCH(sm, {
+        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<SMC>), kBlock, 0);
+        if (r == hipSuccess)
+            r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<SMC>), kBlock, 0);
+    });
     return r;
 }
 
