@@ -430,6 +430,30 @@ inline TakePhotoSettings Camera::take_photo() const { return TakePhotoSettings(*
 // src/bin/raysnail.rs:176-208 combine_pixel: keep old where new is [0,0,0,0], else (old p + new)/(p + 1)
 void combine_pixels(std::vector<Pixel>& old_pixels, const std::vector<Pixel>& new_pixels, float pass);
 
+// ---------------------------------------------------------------- progressive passes + output ----
+// The CLI's pass loop (src/bin/raysnail.rs:311-427, parse_and_render): `passes` frames of
+// `samples` spp at `depth`, each combined into the running image with combine_pixels; after each
+// pass the noise map (calc_noise >= 0.01 on the combined image) is computed on the GPU and
+// reported. Upstream the redo map never reaches the PixelController (the RedoController is built
+// from the initial all-ones map before the loop, raysnail.rs:369-372), so every pass renders
+// every pixel; `adaptive = true` applies each pass's map to the next pass instead.
+struct PassReport {
+    float noise_min = 0.f, noise_max = 0.f;  // raysnail.rs:394-407
+    uint64_t oversample = 0;                  // pixels the redo map marks (raysnail.rs:411-422)
+    rs_render_stats stats{};
+};
+struct ProgressiveResult {
+    std::vector<Pixel> pixels;
+    std::vector<PassReport> passes;
+};
+ProgressiveResult render_passes(const Camera& camera, World& world, size_t samples, size_t passes, uint64_t seed,
+                                bool adaptive = false, size_t depth = 8);
+
+// raysnail.rs:429-441: clamp(c, 0..1) * 255.5 -> u8, RGB rows top first
+std::vector<uint8_t> quantize_rgb8(const std::vector<Pixel>& pixels);
+// 8-bit RGB PNG (stored deflate blocks: no compression library needed); throws Error on I/O failure
+void write_png(const std::string& path, size_t width, size_t height, const std::vector<uint8_t>& rgb);
+
 // -------------------------------------------------------------------------------------- SDL ----
 struct CameraData {  // src/sdl_parser.rs:52-57
     Vec3 location, look_at;
@@ -467,5 +491,11 @@ int rsh_sdl_build(const char* path, uint32_t width, uint32_t height, const raysn
                   rs_camera_desc* cam_out);
 int rsh_sdl_render(const char* path, uint32_t width, uint32_t height, const rs_render_settings* st, float* out_rgba,
                    rs_render_stats* stats);
+/* The CLI's pass loop on an SDL scene (render_passes): the combined RGBA image, and per pass
+ * [noise_min, noise_max, oversample count] in noise_out (3 * passes floats; may be NULL). */
+int rsh_sdl_render_passes(const char* path, uint32_t width, uint32_t height, uint32_t samples, uint32_t passes,
+                          uint64_t seed, int adaptive, float* out_rgba, float* noise_out);
+/* quantize_rgb8 + write_png of a W*H RGBA f32 image */
+int rsh_write_png(const char* path, const float* rgba, uint32_t width, uint32_t height);
 const char* rsh_last_error(void);
 }

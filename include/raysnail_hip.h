@@ -209,6 +209,28 @@ int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* 
 int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st,
                      const uint8_t* d_mask, float* d_out_rgba, void* stream, rs_render_stats* stats);
 
+/* ---- progressive passes (the CLI's pass loop, src/bin/raysnail.rs:311-427) ----
+ * Device-resident frames (RGBA f32, W*H*4), all work on the caller's stream (NULL = default). */
+typedef struct rs_noise_stats {
+    float    min;        /* min over pixels of calc_noise, starting from 3.0 (raysnail.rs:396) */
+    float    max;        /* max, starting from 1.0 (raysnail.rs:397) */
+    uint64_t count;      /* pixels with noise >= threshold: the redo map's ones (raysnail.rs:411-422) */
+} rs_noise_stats;
+
+/* combine_pixels (raysnail.rs:176-208): acc[i] = new[i] == [0,0,0,0] ? acc[i]
+ * : (acc[i] * pass + new[i]) / (pass + 1), per channel in f32. */
+int rs_combine_pixels_device(float* d_acc_rgba, const float* d_new_rgba, uint64_t n_pixels, float pass, void* stream);
+
+/* calc_noise (raysnail.rs:150-173) for every pixel -- including upstream's `let x = y` (the 5x5
+ * window is centred on column y, the reference colour is pixel (x, y)) -- and the redo map
+ * noise >= threshold (raysnail.rs:404-422; the CLI uses 0.01). d_redo may be NULL. Synchronises
+ * the stream to return the stats. */
+int rs_noise_map_device(const float* d_rgba, uint32_t width, uint32_t height, float threshold, uint8_t* d_redo,
+                        void* stream, rs_noise_stats* stats);
+/* the same on host buffers (uploaded, computed on the GPU, redo map copied back; redo may be NULL) */
+int rs_noise_map(const float* rgba, uint32_t width, uint32_t height, float threshold, uint8_t* redo,
+                 rs_noise_stats* stats);
+
 /* ---- diagnostics (parity probes used by tests/) ---- */
 /* World::hit (world.rs:63-65) for n rays on the device. rays: n*7 doubles (origin, direction,
  * time); out: n*13 doubles = [hit, t1, t2, p.xyz, n.xyz, u, v, outside, material id] (u, v are

@@ -70,6 +70,10 @@ class rs_render_settings(C.Structure):
                 ("row_step", C.c_uint32)]
 
 
+class rs_noise_stats(C.Structure):
+    _fields_ = [("min", C.c_float), ("max", C.c_float), ("count", C.c_uint64)]
+
+
 class rs_render_stats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("ms", C.c_double), ("path_ms", C.c_double),
                 ("launches", C.c_uint32), ("kernel_launches", C.c_uint32), ("kernel_ms", C.c_double),
@@ -131,6 +135,12 @@ def load() -> C.CDLL:
     lib.rs_scene_create.argtypes = [C.POINTER(VP)]
     lib.rs_scene_destroy.argtypes = [VP]
     lib.rs_scene_commit.argtypes = [VP]
+    lib.rs_combine_pixels_device.argtypes = [VP, VP, C.c_uint64, C.c_float, VP]
+    lib.rs_combine_pixels_device.restype = C.c_int
+    lib.rs_noise_map_device.argtypes = [VP, C.c_uint32, C.c_uint32, C.c_float, VP, VP, C.POINTER(rs_noise_stats)]
+    lib.rs_noise_map_device.restype = C.c_int
+    lib.rs_noise_map.argtypes = [VP, C.c_uint32, C.c_uint32, C.c_float, VP, C.POINTER(rs_noise_stats)]
+    lib.rs_noise_map.restype = C.c_int
     lib.rs_probe_samples.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), C.c_uint32,
                                      C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
     lib.rs_probe_samples.restype = C.c_int
@@ -153,5 +163,6 @@ EXPORTED_SYMBOLS = [
     "rs_abi_version", "rs_last_error", "rs_device_count", "rs_stream_key", "rs_scene_create", "rs_scene_destroy",
     "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
     "rs_difference", "rs_transformed", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
-    "rs_scene_commit", "rs_render", "rs_render_device", "rs_probe_world_hit", "rs_probe_samples",
+    "rs_scene_commit", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
+    "rs_probe_world_hit", "rs_probe_samples",
 ]

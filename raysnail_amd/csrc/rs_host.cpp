@@ -1176,6 +1176,66 @@ int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
     });
 }
 
+int rs_combine_pixels_device(float* d_acc, const float* d_new, uint64_t n_pixels, float pass, void* stream) {
+    return run([&] {
+        if (!d_acc || !d_new) throw Error(RS_E_INVALID, "null argument");
+        HIP_OK(launch_combine(d_acc, d_new, n_pixels, pass, (hipStream_t)stream));
+    });
+}
+
+int rs_noise_map_device(const float* d_rgba, uint32_t width, uint32_t height, float threshold, uint8_t* d_redo,
+                        void* stream, rs_noise_stats* stats) {
+    return run([&] {
+        if (!d_rgba) throw Error(RS_E_INVALID, "null argument");
+        if ((uint64_t)width * height > 0x7FFFFFFFull) throw Error(RS_E_INVALID, "frame too large");
+        const hipStream_t st = (hipStream_t)stream;
+        // [0] min bits, [1] max bits (non-negative floats order like their bit patterns), [2..3] count
+        unsigned int* d = nullptr;
+        HIP_OK(hipMalloc((void**)&d, 4 * sizeof(unsigned int)));
+        unsigned int init[4];
+        float fmin0 = 3.0f, fmax0 = 1.0f;  // raysnail.rs:396-397
+        std::memcpy(&init[0], &fmin0, 4);
+        std::memcpy(&init[1], &fmax0, 4);
+        init[2] = init[3] = 0;
+        hipError_t e = hipMemcpyAsync(d, init, sizeof(init), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = launch_noise(d_rgba, (int)width, (int)height, threshold, d_redo, d,
+                             reinterpret_cast<unsigned long long*>(d + 2), st);
+        unsigned int out[4] = {0, 0, 0, 0};
+        if (e == hipSuccess) e = hipMemcpyAsync(out, d, sizeof(out), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        (void)hipFree(d);
+        HIP_OK(e);
+        if (stats) {
+            std::memcpy(&stats->min, &out[0], 4);
+            std::memcpy(&stats->max, &out[1], 4);
+            uint64_t c;
+            std::memcpy(&c, &out[2], 8);
+            stats->count = c;
+        }
+    });
+}
+
+int rs_noise_map(const float* rgba, uint32_t width, uint32_t height, float threshold, uint8_t* redo,
+                 rs_noise_stats* stats) {
+    return run([&] {
+        if (!rgba) throw Error(RS_E_INVALID, "null argument");
+        const size_t n = (size_t)width * height;
+        float* d_px = nullptr;
+        uint8_t* d_redo = nullptr;
+        HIP_OK(hipMalloc((void**)&d_px, n * 4 * sizeof(float) + 16));
+        hipError_t e = hipMalloc((void**)&d_redo, n + 16);
+        if (e == hipSuccess) e = hipMemcpy(d_px, rgba, n * 4 * sizeof(float), hipMemcpyHostToDevice);
+        int rc = RS_OK;
+        if (e == hipSuccess) rc = rs_noise_map_device(d_px, width, height, threshold, d_redo, nullptr, stats);
+        if (e == hipSuccess && rc == RS_OK && redo) e = hipMemcpy(redo, d_redo, n, hipMemcpyDeviceToHost);
+        (void)hipFree(d_px);
+        (void)hipFree(d_redo);
+        HIP_OK(e);
+        if (rc != RS_OK) throw Error(rc, g_last_error);
+    });
+}
+
 int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin, double tmax, double* out) {
     return run([&] {
         S(s);

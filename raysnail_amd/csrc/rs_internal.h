@@ -80,6 +80,9 @@ hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* q
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
 hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
+hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st);
+hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, unsigned int* minmax_bits,
+                        unsigned long long* count, hipStream_t st);
 hipError_t launch_probe_hit(const DScene& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
                             hipStream_t st);
 // acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic).

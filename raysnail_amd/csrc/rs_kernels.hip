@@ -866,6 +866,75 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ 
     reinterpret_cast<float4*>(out)[pix] = o;
 }
 
+// ---- progressive passes (src/bin/raysnail.rs:176-208, 150-173, 394-422) ----
+__global__ __launch_bounds__(kBlock) void k_combine(float4* __restrict__ acc, const float4* __restrict__ nw, uint64_t n,
+                                                   float p) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 v = nw[i];
+    if (v.x == 0.f && v.y == 0.f && v.z == 0.f && v.w == 0.f) return;  // no new data: keep old
+    const float4 o = acc[i];
+    const float d = p + 1.0f;
+    acc[i] = make_float4((o.x * p + v.x) / d, (o.y * p + v.y) / d, (o.z * p + v.z) / d, (o.w * p + v.w) / d);
+}
+
+// one pixel's calc_noise: sum over the 5x5 window of color_diff(def, neighbour), window rows
+// y-2..y+2 (outer) and columns y-2..y+2 (inner; upstream shadows x with y), outside = def
+__device__ __forceinline__ float calc_noise(const float4* px, int x, int y, int w, int h) {
+    const float4 def = px[(size_t)y * w + x];
+    float diff = 0.0f;
+    const int cx = y;
+    for (int yy = y - 2; yy < y + 3; ++yy)
+        for (int xx = cx - 2; xx < cx + 3; ++xx) {
+            float4 q = def;
+            if (xx >= 0 && yy >= 0 && xx < w && yy < h) q = px[(size_t)yy * w + xx];
+            const float rd = def.x - q.x, gd = def.y - q.y, bd = def.z - q.z;
+            diff += rd * rd + gd * gd + bd * bd;
+        }
+    return diff;
+}
+
+__global__ __launch_bounds__(kBlock) void k_noise(const float4* __restrict__ px, int w, int h, float t,
+                                                 uint8_t* __restrict__ redo, unsigned int* __restrict__ mm,
+                                                 unsigned long long* __restrict__ count) {
+    __shared__ unsigned int s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < (uint64_t)w * h) {
+        const int x = (int)(i % w), y = (int)(i / w);
+        const float n = calc_noise(px, x, y, w, h);
+        const bool r = n >= t;
+        if (redo) redo[i] = r ? 1 : 0;
+        if (r) atomicAdd(&s_cnt, 1u);
+        // min / max over non-negative floats (or NaN, which the reference's `<` / `>` skip)
+        if (n == n) {
+            atomicMin(&mm[0], __float_as_uint(n));
+            atomicMax(&mm[1], __float_as_uint(n));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_cnt) atomicAdd(count, (unsigned long long)s_cnt);
+}
+
+hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st) {
+    const uint64_t blocks = (n + kBlock - 1) / kBlock;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_combine, dim3((uint32_t)blocks), dim3(kBlock), 0, st, reinterpret_cast<float4*>(acc),
+                       reinterpret_cast<const float4*>(nw), n, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, unsigned int* mm,
+                        unsigned long long* count, hipStream_t st) {
+    const uint64_t n = (uint64_t)w * h;
+    const uint64_t blocks = (n + kBlock - 1) / kBlock;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_noise, dim3((uint32_t)blocks), dim3(kBlock), 0, st, reinterpret_cast<const float4*>(px), w, h,
+                       t, redo, mm, count);
+    return hipGetLastError();
+}
+
 // Diagnostic: World::hit for a batch of rays (tests/ per-primitive parity probes).
 // rays[i] = o(3) d(3) time; out[i] = hit t1 t2 p(3) n(3) 0 0 outside mat  (13 doubles, oracle layout)
 __global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __restrict__ rays, uint32_t n, double tmin,

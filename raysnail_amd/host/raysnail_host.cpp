@@ -1,7 +1,9 @@
 // libraysnail_host: the C++ host layer (include/raysnail.hpp) over the C-ABI of libraysnail_hip.
 // Object export, World / Camera / TakePhotoSettings, combine_pixels, and the C entry points.
 // The SDL front end lives in sdl_parser.cpp.
+#include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -326,6 +328,114 @@ void combine_pixels(std::vector<Pixel>& old_pixels, const std::vector<Pixel>& ne
     }
 }
 
+ProgressiveResult render_passes(const Camera& camera, World& world, size_t samples, size_t passes, uint64_t seed,
+                                bool adaptive, size_t depth) {
+    const size_t W = camera.picture_width(), H = camera.picture_height();
+    ProgressiveResult res;
+    res.pixels.assign(W * H, Pixel{0.f, 0.f, 0.f, 1.f});  // raysnail.rs:317-322
+    std::vector<uint8_t> redo(W * H, 1);
+    struct Redo : PixelController {  // RedoController, raysnail.rs:123-134
+        const std::vector<uint8_t>* map;
+        size_t width;
+        bool calculate_pixel(size_t x, size_t y) const override { return (*map)[y * width + x] > 0; }
+    } controller;
+    controller.map = &redo;
+    controller.width = W;
+    const std::vector<uint8_t> initial = redo;  // what upstream's controller keeps seeing
+    for (size_t p = 0; p < passes; ++p) {
+        TakePhotoSettings photo = camera.take_photo();
+        photo.samples(samples).depth(depth).seed(seed).pass_index((uint32_t)p);
+        if (!adaptive) controller.map = &initial;
+        std::vector<Pixel> px = photo.shot_to_target(nullptr, world, nullptr, nullptr, &controller);
+        combine_pixels(res.pixels, px, (float)p);
+        PassReport rep;
+        rep.stats = photo.last_stats();
+        rs_noise_stats ns{};
+        check_rs(rs_noise_map(reinterpret_cast<const float*>(res.pixels.data()), (uint32_t)W, (uint32_t)H, 0.01f,
+                              redo.data(), &ns));
+        rep.noise_min = ns.min;
+        rep.noise_max = ns.max;
+        rep.oversample = ns.count;
+        res.passes.push_back(rep);
+        controller.map = &redo;
+    }
+    return res;
+}
+
+std::vector<uint8_t> quantize_rgb8(const std::vector<Pixel>& pixels) {
+    std::vector<uint8_t> out(pixels.size() * 3);
+    for (size_t i = 0; i < pixels.size(); ++i)
+        for (int c = 0; c < 3; ++c) {
+            double v = (double)pixels[i][c];  // clamp(c as f64, 0.0 .. 1.0) * 255.5, `as u8` saturates
+            v = v < 0.0 ? 0.0 : v > 1.0 ? 1.0 : v;
+            if (v != v) v = 0.0;              // Rust's float -> int cast maps NaN to 0
+            const double q = v * 255.5;
+            out[3 * i + c] = (uint8_t)(q >= 255.0 ? 255 : (int)q);
+        }
+    return out;
+}
+
+namespace {
+uint32_t crc32_of(const uint8_t* p, size_t n, uint32_t c = 0xFFFFFFFFu) {
+    static uint32_t table[256];
+    static bool init = false;
+    if (!init) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t k = i;
+            for (int j = 0; j < 8; ++j) k = (k & 1) ? 0xEDB88320u ^ (k >> 1) : k >> 1;
+            table[i] = k;
+        }
+        init = true;
+    }
+    for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    return c;
+}
+void put_be32(std::vector<uint8_t>& v, uint32_t x) {
+    v.push_back((uint8_t)(x >> 24)); v.push_back((uint8_t)(x >> 16)); v.push_back((uint8_t)(x >> 8)); v.push_back((uint8_t)x);
+}
+void chunk(std::vector<uint8_t>& out, const char* type, const std::vector<uint8_t>& data) {
+    put_be32(out, (uint32_t)data.size());
+    std::vector<uint8_t> td(type, type + 4);
+    td.insert(td.end(), data.begin(), data.end());
+    out.insert(out.end(), td.begin(), td.end());
+    put_be32(out, crc32_of(td.data(), td.size()) ^ 0xFFFFFFFFu);
+}
+}  // namespace
+
+void write_png(const std::string& path, size_t width, size_t height, const std::vector<uint8_t>& rgb) {
+    if (rgb.size() != width * height * 3) throw Error(RS_E_INVALID, "write_png: size mismatch");
+    std::vector<uint8_t> raw;  // filter byte 0 + row
+    raw.reserve(height * (width * 3 + 1));
+    for (size_t y = 0; y < height; ++y) {
+        raw.push_back(0);
+        raw.insert(raw.end(), rgb.begin() + y * width * 3, rgb.begin() + (y + 1) * width * 3);
+    }
+    std::vector<uint8_t> z = {0x78, 0x01};  // zlib header, stored blocks of <= 65535 bytes
+    uint32_t a = 1, b = 0;
+    for (size_t i = 0; i < raw.size(); i += 65535) {
+        const size_t n = std::min<size_t>(65535, raw.size() - i);
+        z.push_back(i + n >= raw.size() ? 1 : 0);
+        z.push_back((uint8_t)n); z.push_back((uint8_t)(n >> 8));
+        z.push_back((uint8_t)~n); z.push_back((uint8_t)(~n >> 8));
+        z.insert(z.end(), raw.begin() + i, raw.begin() + i + n);
+    }
+    for (uint8_t c : raw) { a = (a + c) % 65521; b = (b + a) % 65521; }  // adler32
+    put_be32(z, (b << 16) | a);
+    std::vector<uint8_t> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+    std::vector<uint8_t> ihdr;
+    put_be32(ihdr, (uint32_t)width);
+    put_be32(ihdr, (uint32_t)height);
+    ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});  // 8-bit RGB
+    chunk(png, "IHDR", ihdr);
+    chunk(png, "IDAT", z);
+    chunk(png, "IEND", {});
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw Error(RS_E_INVALID, "cannot write " + path);
+    const size_t wr = std::fwrite(png.data(), 1, png.size(), f);
+    std::fclose(f);
+    if (wr != png.size()) throw Error(RS_E_INVALID, "short write to " + path);
+}
+
 CliScene cli_scene(SceneData scene, size_t width, size_t height) {
     if (!scene.camera) throw Error(RS_E_INVALID, "scene has no camera");  // scene_data.camera.unwrap()
     const CameraData& cd = *scene.camera;
@@ -398,6 +508,31 @@ extern "C" int rsh_sdl_render(const char* path, uint32_t width, uint32_t height,
         std::vector<Pixel> px = photo.shot(nullptr, sc.world);
         std::memcpy(out_rgba, px.data(), px.size() * sizeof(Pixel));
         if (stats) *stats = photo.last_stats();
+    });
+}
+
+extern "C" int rsh_sdl_render_passes(const char* path, uint32_t width, uint32_t height, uint32_t samples,
+                                     uint32_t passes, uint64_t seed, int adaptive, float* out_rgba, float* noise_out) {
+    return guarded([&] {
+        if (!path || !out_rgba) throw Error(RS_E_INVALID, "null argument");
+        CliScene sc = cli_scene(SdlParser::parse(path), width, height);
+        ProgressiveResult r = render_passes(sc.camera, sc.world, samples, passes, seed, adaptive != 0);
+        std::memcpy(out_rgba, r.pixels.data(), r.pixels.size() * sizeof(Pixel));
+        if (noise_out)
+            for (size_t p = 0; p < r.passes.size(); ++p) {
+                noise_out[3 * p] = r.passes[p].noise_min;
+                noise_out[3 * p + 1] = r.passes[p].noise_max;
+                noise_out[3 * p + 2] = (float)r.passes[p].oversample;
+            }
+    });
+}
+
+extern "C" int rsh_write_png(const char* path, const float* rgba, uint32_t width, uint32_t height) {
+    return guarded([&] {
+        if (!path || !rgba) throw Error(RS_E_INVALID, "null argument");
+        std::vector<Pixel> px((size_t)width * height);
+        std::memcpy(px.data(), rgba, px.size() * sizeof(Pixel));
+        write_png(path, width, height, quantize_rgb8(px));
     });
 }
 

@@ -9,6 +9,8 @@ these two C entry points expose it to Python:
   returns the camera.
 * ``sdl_render(path, width, height, settings)`` -- the same scene rendered on the GPU through the
   C++ World / TakePhotoSettings path. Raises if the library is missing: there is no fallback.
+* ``sdl_render_passes(...)`` -- the CLI's progressive pass loop (render_passes); ``write_png`` --
+  the CLI's quantisation (clamp * 255.5 -> u8) and PNG output.
 """
 from __future__ import annotations
 
@@ -57,6 +59,11 @@ def load() -> C.CDLL:
     lib.rsh_sdl_render.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(A.rs_render_settings), C.c_void_p,
                                    C.POINTER(A.rs_render_stats)]
     lib.rsh_sdl_render.restype = C.c_int
+    lib.rsh_sdl_render_passes.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                          C.c_int, C.c_void_p, C.c_void_p]
+    lib.rsh_sdl_render_passes.restype = C.c_int
+    lib.rsh_write_png.argtypes = [C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32]
+    lib.rsh_write_png.restype = C.c_int
     lib.rsh_last_error.restype = C.c_char_p
     _LIB = lib
     return lib
@@ -85,3 +92,19 @@ def sdl_render(path: str, width: int, height: int, settings: A.rs_render_setting
     _check(load().rsh_sdl_render(os.fsencode(path), width, height, C.byref(settings),
                                  out.ctypes.data_as(C.c_void_p), C.byref(stats)))
     return out, stats
+
+
+def sdl_render_passes(path: str, width: int, height: int, samples: int, passes: int, seed: int,
+                      adaptive: bool = False):
+    """The CLI's pass loop (render_passes): combined image and per-pass [noise min, max, count]."""
+    out = np.zeros((height, width, 4), dtype=np.float32)
+    noise = np.zeros((passes, 3), dtype=np.float32)
+    _check(load().rsh_sdl_render_passes(os.fsencode(path), width, height, samples, passes, seed, int(adaptive),
+                                        out.ctypes.data_as(C.c_void_p), noise.ctypes.data_as(C.c_void_p)))
+    return out, noise
+
+
+def write_png(path: str, rgba: np.ndarray) -> None:
+    rgba = np.ascontiguousarray(rgba, dtype=np.float32)
+    h, w = rgba.shape[:2]
+    _check(load().rsh_write_png(os.fsencode(path), rgba.ctypes.data_as(C.c_void_p), w, h))
