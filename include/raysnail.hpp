@@ -58,16 +58,83 @@ struct Color {  // src/prelude/color.rs:11-47 (f32 rgba)
     }
 };
 
+// -------------------------------------------------------------------------------- FastRng ----
+// src/prelude/random.rs:109-145: XorShiftRng (rand_xorshift 0.3.0) seeded by rand_core 0.6's
+// seed_from_u64. The reference seeds it from the OS (FastRng::new); here the seed is explicit.
+class FastRng {
+public:
+    explicit FastRng(uint64_t seed);
+    uint32_t next_u32();
+    uint64_t next_u64();
+    double gen();                          // next_u64 as f64 / u64::MAX as f64, in [0, 1]
+    double range(double start, double end) { return start + gen() * (end - start); }
+    // rand 0.8.3 SliceRandom::shuffle: for i in (1..len).rev() swap(i, gen_range(0..i+1)), with
+    // UniformInt<u32>::sample_single's widening-multiply rejection (third-party, restated)
+    void shuffle(std::vector<uint32_t>& v);
+    uint32_t gen_index(uint32_t ubound);
+private:
+    uint32_t x_, y_, z_, w_;
+};
+
 // ---------------------------------------------------------------------------------- textures ----
-// Arc<dyn Texture>: a solid Color (color.rs:61-65) or a Checker (texture/checker.rs:13-30).
+enum class SmoothType { None = RS_SMOOTH_NONE, LinearInterpolate = RS_SMOOTH_LINEAR, HermitianCubic = RS_SMOOTH_HERMITE };
+
+struct PerlinData {  // the tables of texture/noise.rs:28-37 + the texture settings
+    uint32_t point_count = 0;
+    bool vector = false;
+    SmoothType smooth = SmoothType::HermitianCubic;
+    int32_t type = RS_PERLIN_NORMAL;
+    uint32_t depth = 0;
+    double scale = 1.0;
+    std::vector<double> values;                    // 3 per point (Vector) or 1 (Float)
+    std::vector<uint32_t> perm_x, perm_y, perm_z;
+};
+
+class Perlin {  // src/texture/noise.rs
+public:
+    // Perlin::new (noise.rs:44-66): values Vec3::random_unit / gen, then three shuffled permutations
+    Perlin(size_t point_count, bool vector, FastRng& rng);
+    Perlin& scale(double s) { d_->scale = s; return *this; }
+    Perlin& smooth(SmoothType t) { d_->smooth = t; return *this; }
+    Perlin& turbulence(uint8_t depth) { d_->type = RS_PERLIN_TURBULENCE; d_->depth = depth; return *this; }
+    Perlin& marble(uint8_t depth) { d_->type = RS_PERLIN_MARBLE; d_->depth = depth; return *this; }
+    const std::shared_ptr<PerlinData>& data() const { return d_; }
+private:
+    std::shared_ptr<PerlinData> d_;
+};
+
+struct ImageData {  // decoded 8-bit RGB, row 0 = top
+    uint32_t width = 0, height = 0;
+    std::vector<uint8_t> rgb;
+};
+
+class Image {  // src/texture/image.rs
+public:
+    // Image::new (image.rs:24-31): decodes a PNG (8-bit gray / gray-alpha / RGB / RGBA / palette,
+    // non-interlaced); throws Error like the reference's Err(String)
+    static Image open(const std::string& path);
+    Image(uint32_t width, uint32_t height, std::vector<uint8_t> rgb);
+    const std::shared_ptr<const ImageData>& data() const { return d_; }
+private:
+    std::shared_ptr<const ImageData> d_;
+};
+
+// Arc<dyn Texture>: a solid Color (color.rs:61-65), a Checker (texture/checker.rs:13-30), a Perlin
+// noise (texture/noise.rs) or an Image (texture/image.rs).
 struct Texture {
     int32_t kind = RS_TEX_SOLID;
     Color odd, even;
     double scale = 1.0;
+    std::shared_ptr<const PerlinData> perlin;
+    std::shared_ptr<const ImageData> image;
     static Texture color(const Color& c) { Texture t; t.kind = RS_TEX_SOLID; t.odd = t.even = c; return t; }
     static Texture checker(const Color& odd, const Color& even, double scale) {
         Texture t; t.kind = RS_TEX_CHECKER; t.odd = odd; t.even = even; t.scale = scale; return t;
     }
+    static Texture noise(const Perlin& p) {
+        Texture t; t.kind = RS_TEX_PERLIN; t.perlin = std::make_shared<const PerlinData>(*p.data()); return t;
+    }
+    static Texture of(const Image& i) { Texture t; t.kind = RS_TEX_IMAGE; t.image = i.data(); return t; }
 };
 
 class SceneSink;
@@ -85,7 +152,7 @@ public:
     virtual CommonMaterialSettings settings() const { return settings_; }
     void set(const CommonMaterialSettings& s) { settings_ = s; }
 protected:
-    rs_material_desc base_desc(int32_t kind, const Texture& t) const;
+    rs_material_desc base_desc(SceneSink& sink, int32_t kind, const Texture& t) const;
     CommonMaterialSettings settings_;
 };
 using MaterialRef = std::shared_ptr<const Material>;
@@ -136,6 +203,23 @@ public:
 private:
     Texture tex_;
     double mult_ = 1.0;
+};
+
+class Isotropic : public Material {  // src/material/isotropic.rs
+public:
+    explicit Isotropic(Color c) : color_(c) {}
+    int32_t export_to(SceneSink& sink) const override;
+private:
+    Color color_;
+};
+
+class BlinnPhong : public Material {  // src/material/blinn_phong.rs
+public:
+    BlinnPhong(double k_specular, double exponent, Texture t) : k_(k_specular), e_(exponent), tex_(t) {}
+    int32_t export_to(SceneSink& sink) const override;
+private:
+    double k_, e_;
+    Texture tex_;
 };
 
 class MixedMaterial : public Material {  // src/material/mixed_material.rs
@@ -212,8 +296,17 @@ private:
 
 class TriangleMesh : public Hittable {  // src/hittable/geometry/triangle_mesh.rs (one Triangle per face)
 public:
-    // positions: 9 doubles per triangle; normals: 9 per triangle or empty (face normals)
+    // positions: 9 doubles per triangle; normals: 9 per triangle or empty (zero normals)
     TriangleMesh(std::vector<double> positions, std::vector<double> normals, MaterialRef mat);
+    // TriangleMesh::load (triangle_mesh.rs:166-276): an OBJ file through a tobj-4.0.2-compatible
+    // reader (single_index, triangulate), each vertex rotated about `axis` by rotation_angle degrees,
+    // then p * scale + offset; vertex normals from the file (rotated) or the averaged unit face
+    // normals of the rotated positions
+    static std::shared_ptr<TriangleMesh> load(const std::string& filename, double scale, Vec3 offset,
+                                              double rotation_angle, int axis, MaterialRef material);
+    size_t len() const { return pos_.size() / 9; }
+    const std::vector<double>& positions() const { return pos_; }
+    const std::vector<double>& normals() const { return nrm_; }
     std::vector<uint32_t> export_to(SceneSink& sink) const override;
 private:
     std::vector<double> pos_, nrm_;
@@ -264,6 +357,31 @@ private:
     std::vector<rs_transform> stack_;
 };
 
+class ConstantMedium : public Hittable {  // src/hittable/medium/constant.rs (material Isotropic(color))
+public:
+    ConstantMedium(HittableRef boundary, Color color, double density)
+        : boundary_(std::move(boundary)), color_(color), density_(density) {}
+    std::vector<uint32_t> export_to(SceneSink& sink) const override;
+private:
+    HittableRef boundary_;
+    Color color_;
+    double density_;
+};
+
+class HittableList;
+
+// A BVH (or HittableList) used as one object of another list (bvh.rs, list.rs). The device scene
+// has one BVH over every object, so a group exports its members; a TfFacade of a group becomes a
+// TfFacade of each member (the same closest hit for spheres / rects / triangles; for
+// order-dependent members the group's own BVH order is not kept).
+class BVH : public Hittable {
+public:
+    BVH(const HittableList& list, std::pair<double, double> time_limit = {0.0, 0.0});
+    std::vector<uint32_t> export_to(SceneSink& sink) const override;
+private:
+    std::vector<HittableRef> objects_;
+};
+
 class TfFacade : public Hittable {  // src/hittable/transform/tf_facade.rs
 public:
     TfFacade(HittableRef obj, TransformStack stack) : obj_(std::move(obj)), stack_(std::move(stack)) {}
@@ -307,6 +425,9 @@ typedef struct rsh_sink_api {
     int (*lights_add)(void* s, uint32_t h);
     int (*set_background)(void* s, const float* lo, const float* hi);
     int (*set_time_range)(void* s, double t0, double t1);
+    int (*perlin)(void* s, const rs_perlin_desc* d, int32_t* id);
+    int (*image)(void* s, const uint8_t* rgb, uint32_t w, uint32_t h, int32_t* id);
+    int (*constant_medium)(void* s, uint32_t boundary, const float* color, double density, uint32_t* h);
     const char* (*last_error)(void);
 } rsh_sink_api;
 }
@@ -320,6 +441,8 @@ public:
     const rsh_sink_api& api;
     void* scene;
     std::unordered_map<const void*, int32_t> materials;              // exported once each
+    std::unordered_map<const void*, int32_t> textures;               // Perlin / Image data, once each
+    int32_t texture_data(const Texture& t);
     std::unordered_map<const void*, std::vector<uint32_t>> objects;
     int32_t material(const MaterialRef& m);
     std::vector<uint32_t> object(const HittableRef& o);
@@ -495,6 +618,14 @@ int rsh_sdl_render(const char* path, uint32_t width, uint32_t height, const rs_r
  * [noise_min, noise_max, oversample count] in noise_out (3 * passes floats; may be NULL). */
 int rsh_sdl_render_passes(const char* path, uint32_t width, uint32_t height, uint32_t samples, uint32_t passes,
                           uint64_t seed, int adaptive, float* out_rgba, float* noise_out);
+/* TriangleMesh::load: *n triangles, *pos and *nrm = malloc'd 9 doubles per triangle (free with rsh_free) */
+int rsh_obj_load(const char* path, double scale, const double offset[3], double rotation_angle, int axis,
+                 uint32_t* n, double** pos, double** nrm);
+/* Perlin::new(point_count, vector, FastRng(seed)): values (3 or 1 per point) and perm_x|perm_y|perm_z */
+int rsh_perlin_tables(uint64_t seed, uint32_t point_count, int vector, double* values, uint32_t* perms);
+/* Image::new: decoded 8-bit RGB (*rgb malloc'd, free with rsh_free) */
+int rsh_png_load(const char* path, uint32_t* width, uint32_t* height, uint8_t** rgb);
+void rsh_free(void* p);
 /* quantize_rgb8 + write_png of a W*H RGBA f32 image */
 int rsh_write_png(const char* path, const float* rgba, uint32_t width, uint32_t height);
 const char* rsh_last_error(void);

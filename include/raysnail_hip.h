@@ -15,8 +15,10 @@
  *   rs_material              Lambertian/Metal/DiffuseMetal/Dielectric/DiffuseLight/MixedMaterial
  *                            constructors                      src/material/{lambertian.rs:29-35,
  *                            metal.rs:43-49 (DiffuseMetal), metal.rs:95-100 (Metal), dielectric.rs:38-53,
- *                            light.rs:17-28, mixed_material.rs:32-38}; textures Color / Checker
- *                            src/prelude/color.rs:61-65, src/texture/checker.rs:16-18;
+ *                            light.rs:17-28, mixed_material.rs:32-38, isotropic.rs:15-22,
+ *                            blinn_phong.rs:19-28}; textures Color / Checker / Perlin / Image
+ *                            src/prelude/color.rs:61-65, src/texture/checker.rs:16-18,
+ *                            src/texture/noise.rs, src/texture/image.rs;
  *                            CommonMaterialSettings src/material/mod.rs:41-54
  *   rs_sphere                Sphere::new / with_speed         src/hittable/geometry/sphere.rs:35-48
  *   rs_aarect                AARect::new_xy/new_xz/new_yz     src/hittable/geometry/rect.rs:58-79
@@ -27,6 +29,10 @@
  *   rs_difference            Difference::new                  src/hittable/csg/difference.rs:32-38
  *   rs_transformed           TfFacade::new + TransformStack   src/hittable/transform/tf_facade.rs:30-37,
  *                                                             transform.rs:16-127
+ *   rs_constant_medium       ConstantMedium::new (+ Isotropic) src/hittable/medium/constant.rs:29-39,
+ *                                                             src/material/isotropic.rs:15-22
+ *   rs_perlin                Perlin::new/scale/smooth/turbulence/marble  src/texture/noise.rs:44-103
+ *   rs_image                 Image::new (decoded pixels)      src/texture/image.rs:24-31
  *   rs_world_add             HittableList::add (world list)   src/hittable/collection/list.rs:29-33
  *   rs_lights_add            HittableList::add (lights list)  src/hittable/collection/list.rs:29-33
  *   rs_set_background        World background closure         examples/rtow_13_1.rs:38-41,
@@ -47,7 +53,11 @@
  * (painter.rs:167-170), Camera::ray disk rejection + shutter time (camera.rs:77-85), then per
  * bounce of ray_color (camera.rs:156-255). thread_rng draws on the path are taken from the same
  * stream at the same point: Dielectric's Random::normal (dielectric.rs:72) as one gen(),
- * MixedMaterial's next_u32 (mixed_material.rs:44) as one next_u32().
+ * MixedMaterial's next_u32 (mixed_material.rs:44) as one next_u32(). ConstantMedium::hit's
+ * Random::normal() (medium/constant.rs:63) is called inside world.hit, where the number of calls
+ * depends on the traversal; it is therefore NOT taken from the stream but from a counter-free hash
+ * of the stream's state at the start of the segment and the medium's handle (rs_medium_uniform),
+ * so every test of one medium within one world.hit sees the same draw, on every backend.
  */
 #ifndef RAYSNAIL_HIP_H
 #define RAYSNAIL_HIP_H
@@ -58,7 +68,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 1
+#define RS_ABI_VERSION 2
 
 /* ---- status codes ---- */
 #define RS_OK             0
@@ -69,12 +79,14 @@ extern "C" {
 #define RS_E_UNSUPPORTED -5  /* construct outside what the GPU path implements */
 #define RS_E_NOMEM       -6
 
-/* ---- textures (src/prelude/color.rs:61-65, src/texture/checker.rs:21-30) ---- */
+/* ---- textures (src/prelude/color.rs:61-65, src/texture/{checker.rs:21-30, noise.rs, image.rs}) ---- */
 #define RS_TEX_SOLID   0
 #define RS_TEX_CHECKER 1
+#define RS_TEX_PERLIN  2  /* data = rs_perlin id; Color(1,1,1,1) * noise (noise.rs:187-211) */
+#define RS_TEX_IMAGE   3  /* data = rs_image id; pixel at (u W, (1 - v) H) / 255 (image.rs:34-50) */
 typedef struct rs_texture_desc {
     int32_t kind;     /* RS_TEX_SOLID: color = even; RS_TEX_CHECKER: sin(sx)sin(sy)sin(sz) < 0 ? odd : even */
-    int32_t _pad;
+    int32_t data;     /* RS_TEX_PERLIN / RS_TEX_IMAGE: the id returned by rs_perlin / rs_image */
     float   even[4];  /* rgba */
     float   odd[4];   /* rgba */
     double  scale;    /* checker frequency */
@@ -87,6 +99,8 @@ typedef struct rs_texture_desc {
 #define RS_MAT_DIELECTRIC    3
 #define RS_MAT_DIFFUSE_LIGHT 4
 #define RS_MAT_MIXED         5
+#define RS_MAT_ISOTROPIC     6  /* Isotropic(color = texture.even): SpherePdf (isotropic.rs:25-33) */
+#define RS_MAT_BLINN_PHONG   7  /* BlinnPhong(k_specular, exponent, texture): BlinnPhongPdf (blinn_phong.rs:32-42) */
 #define RS_NO_MATERIAL      (-1)  /* Option<Arc<dyn Material>> = None */
 
 typedef struct rs_material_desc {
@@ -94,14 +108,39 @@ typedef struct rs_material_desc {
     int32_t glass;            /* Dielectric: 1 = .reflect_curve(Glass{}) (Schlick), 0 = none */
     rs_texture_desc texture;  /* albedo / light texture; Dielectric tint = texture.even */
     double  refractive;       /* Dielectric refractive index */
-    double  exponent;         /* DiffuseMetal phong-lobe exponent */
+    double  exponent;         /* DiffuseMetal phong-lobe exponent; BlinnPhong exponent */
     double  multiplier;       /* DiffuseLight multiplier */
     int32_t mix_a, mix_b;     /* MixedMaterial: material ids (already created) */
     double  mix_p;            /* MixedMaterial probability of mix_a */
     double  phong_factor;     /* CommonMaterialSettings.phong_factor (0 = off) */
     int32_t phong_exponent;   /* CommonMaterialSettings.phong_exponent */
     int32_t _pad;
+    double  k_specular;       /* BlinnPhong k_specular */
 } rs_material_desc;
+
+/* ---- Perlin noise texture data (src/texture/noise.rs) ----
+ * The reference builds the tables from a FastRng seeded by the OS (noise.rs:44-66 via
+ * FastRng::new()); here the caller passes the tables (include/raysnail.hpp builds them from a
+ * seeded FastRng with rand 0.8's shuffle). */
+#define RS_PERLIN_NORMAL     0  /* TextureType::Normal: noise(scale p), (n + 1) / 2 for vector values */
+#define RS_PERLIN_TURBULENCE 1  /* TextureType::Turbulence(depth) */
+#define RS_PERLIN_MARBLE     2  /* TextureType::Marble(depth): (sin(scale z + 10 turb) + 1) / 2 */
+#define RS_SMOOTH_NONE       0
+#define RS_SMOOTH_LINEAR     1
+#define RS_SMOOTH_HERMITE    2
+typedef struct rs_perlin_desc {
+    uint32_t        point_count;  /* power of two (indices are masked with point_count - 1) */
+    int32_t         vector;       /* 1: RandomValueType::Vector (values = 3 doubles each), 0: Float */
+    int32_t         smooth;       /* RS_SMOOTH_* */
+    int32_t         type;         /* RS_PERLIN_* */
+    uint32_t        depth;        /* turbulence / marble depth */
+    int32_t         _pad;
+    double          scale;
+    const double*   values;       /* point_count * (vector ? 3 : 1) */
+    const uint32_t* perm_x;       /* point_count each, entries < point_count */
+    const uint32_t* perm_y;
+    const uint32_t* perm_z;
+} rs_perlin_desc;
 
 /* ---- geometry ---- */
 #define RS_PLANE_XY 0   /* AARect::new_xy: axes (0,1), fixed 2 */
@@ -171,10 +210,17 @@ int         rs_abi_version(void);
 const char* rs_last_error(void);
 int         rs_device_count(int* count);
 uint64_t    rs_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample);
+/* ConstantMedium's Random::normal(): a uniform in [0, 1] from the XorShift128 state (x, y, z, w)
+ * at the start of the segment and the medium's handle (see the determinism contract above) */
+double      rs_medium_uniform(const uint32_t state[4], uint32_t handle);
 
 /* ---- scene construction ---- */
 int rs_scene_create(rs_scene** out);
 int rs_scene_destroy(rs_scene* s);
+/* texture data referenced by rs_texture_desc.data */
+int rs_perlin(rs_scene* s, const rs_perlin_desc* desc, int32_t* id_out);
+/* decoded 8-bit RGB pixels, row 0 = top (what DynamicImage::get_pixel indexes, image.rs:34-50) */
+int rs_image(rs_scene* s, const uint8_t* rgb, uint32_t width, uint32_t height, int32_t* id_out);
 int rs_material(rs_scene* s, const rs_material_desc* desc, int32_t* id_out);
 int rs_sphere(rs_scene* s, const double center[3], double radius, const double speed[3] /* NULL = 0 */,
               int32_t material, uint32_t* handle_out);
@@ -190,6 +236,8 @@ int rs_triangles(rs_scene* s, const double* pos, const double* nrm, uint32_t n, 
 int rs_intersection(rs_scene* s, uint32_t a, uint32_t b, int32_t material, uint32_t* handle_out);
 int rs_difference(rs_scene* s, uint32_t plus, uint32_t minus, int32_t material, uint32_t* handle_out);
 int rs_transformed(rs_scene* s, uint32_t object, const rs_transform* stack, uint32_t n, uint32_t* handle_out);
+/* ConstantMedium::new(boundary, color, density): the medium's material is Isotropic(color) */
+int rs_constant_medium(rs_scene* s, uint32_t boundary, const float color[4], double density, uint32_t* handle_out);
 int rs_world_add(rs_scene* s, uint32_t handle);
 int rs_lights_add(rs_scene* s, uint32_t handle);
 int rs_set_background(rs_scene* s, const float lo[3], const float hi[3]);
@@ -234,7 +282,8 @@ int rs_noise_map(const float* rgba, uint32_t width, uint32_t height, float thres
 /* ---- diagnostics (parity probes used by tests/) ---- */
 /* World::hit (world.rs:63-65) for n rays on the device. rays: n*7 doubles (origin, direction,
  * time); out: n*13 doubles = [hit, t1, t2, p.xyz, n.xyz, u, v, outside, material id] (u, v are
- * not computed on the GPU: 0). tmax must be +inf or the hit is dropped when t1 >= tmax. */
+ * computed only in scenes with an Image texture, the only reader: 0 otherwise). The medium key of
+ * the probe rays is 0. tmax must be +inf or the hit is dropped when t1 >= tmax. */
 int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin, double tmax, double* out);
 
 /* Radiance of samples s0 .. s0+n-1 of pixel (x, y) -- one ray_color (camera.rs:156-255) each, the

@@ -19,8 +19,11 @@
 //   Sphere, AARect, Box, Quadric, Triangle                                src/hittable/geometry/*.rs
 //   Intersection, Difference                                              src/hittable/csg/*.rs
 //   TfFacade, Transform, TransformStack                                   src/hittable/transform/*.rs
-//   Lambertian, Metal, DiffuseMetal, Dielectric(+Glass), DiffuseLight, MixedMaterial  src/material/*.rs
-//   Checker texture                                                       src/texture/checker.rs:21-30
+//   Lambertian, Metal, DiffuseMetal, Dielectric(+Glass), DiffuseLight, MixedMaterial,
+//   Isotropic, BlinnPhong                                                 src/material/*.rs
+//   SpherePdf, BlinnPhongPdf, Vec3::random_unit                           src/prelude/pdf.rs:144-238, vec3.rs:91-96
+//   ConstantMedium                                                        src/hittable/medium/constant.rs
+//   Checker, Perlin, Image textures                                       src/texture/{checker.rs:21-30, noise.rs, image.rs:34-50}
 //
 // Deviations, all documented in DESIGN.md §Oracle:
 //   * RNG: the reference seeds every FastRng from the OS (thread_rng). Here sample s of pixel p
@@ -34,6 +37,10 @@
 //   * Box::hit with >= 3 face hits aborts upstream (assert, box.rs:129); here the first two are used.
 //   * Unbounded rejection loops (disk, Sphere::random, ReflectionPdf::generate) are capped at
 //     RS_REJECTION_CAP tries, identically in the GPU path; the cap is never reached in practice.
+//   * ConstantMedium::hit draws Random::normal() from thread_rng inside world.hit; here the draw is
+//     a hash of the segment's stream state and the medium's handle (medium_uniform), so it does not
+//     depend on how often the traversal tests the medium. ConstantMedium::contains panics upstream
+//     (unimplemented!); here it returns false.
 //
 // Pinning: the reference (Rust) cannot be built or run in this container and ships no golden
 // data. The restatement is pinned by the reference's own transform test (transform.rs:187-206, as a
@@ -124,6 +131,7 @@ static inline Vec3 color_to_vec(const Color& c) { return Vec3((double)c.r, (doub
 struct Ray {
     Vec3 origin, direction;
     double time = 0;
+    uint64_t key = 0;  // the segment's medium key (medium_uniform); carried through TfFacade
     Ray() = default;
     Ray(const Vec3& o, const Vec3& d, double t) : origin(o), direction(d), time(t) {}
     // ray.rs:21-31 per-axis mul_add
@@ -181,6 +189,13 @@ static inline uint64_t splitmix64(uint64_t x) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+// the medium key of a segment: a hash of the stream state, not a draw (rs_device.h Rng::medium_key)
+static inline uint64_t medium_key(const FastRng& r) {
+    return splitmix64((((uint64_t)r.y << 32) | r.x) ^ splitmix64(((uint64_t)r.w << 32) | r.z));
+}
+static inline double medium_uniform(uint64_t key, uint32_t handle) {
+    return (double)splitmix64(key ^ splitmix64(0x6d656469756d2121ULL + (uint64_t)handle)) * 0x1p-64;
+}
 static inline uint64_t stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
     uint64_t k = splitmix64(seed);
     k = splitmix64(k ^ (uint64_t)pass);
@@ -204,12 +219,20 @@ static Vec3 random_unit_disk(FastRng& rng) {
 // this file calls glibc instead (liboracle_glibc.so), to measure what that choice changes.
 #ifdef ORC_GLIBC_MATH
 static inline void lm_sincos(double x, double* s, double* c) { *s = std::sin(x); *c = std::cos(x); }
+static inline double lm_sin(double x) { return std::sin(x); }
 static inline double lm_pow(double x, double y) { return std::pow(x, y); }
 static inline bool lm_sin3_negative(double a, double b, double c) { return std::sin(a) * std::sin(b) * std::sin(c) < 0.0; }
+static inline double lm_log(double x) { return std::log(x); }
+static inline double lm_atan2(double y, double x) { return std::atan2(y, x); }
+static inline double lm_asin(double x) { return std::asin(x); }
 #else
 static inline void lm_sincos(double x, double* s, double* c) { rs_cr::sincos_cr(x, s, c); }
+static inline double lm_sin(double x) { return rs_cr::sin_cr(x); }
 static inline double lm_pow(double x, double y) { return rs_cr::pow_cr(x, y); }
 static inline bool lm_sin3_negative(double a, double b, double c) { return rs_cr::sin3_negative(a, b, c); }
+static inline double lm_log(double x) { return rs_cr::log_cr(x); }
+static inline double lm_atan2(double y, double x) { return rs_cr::atan2_cr(y, x); }
+static inline double lm_asin(double x) { return rs_cr::asin_cr(x); }
 #endif
 
 // vec3.rs:100-111
@@ -231,6 +254,16 @@ static Vec3 random_cosine_direction_exponent(double exponent, FastRng& rng) {
     double sp, cp;
     lm_sincos(phi, &sp, &cp);
     return Vec3(cp * sin_theta, sp * sin_theta, r2);
+}
+
+// vec3.rs:91-96
+static Vec3 random_unit(FastRng& rng) {
+    double a = rng.range(0.0, 2.0 * PI);
+    double z = rng.range(-1.0, 1.0);
+    double r = std::sqrt(1.0 - z * z);
+    double sa, ca;
+    lm_sincos(a, &sa, &ca);
+    return Vec3(r * ca, r * sa, z);
 }
 
 // ---------------------------------------------------------------- ONB (onb.rs) ----
@@ -257,26 +290,52 @@ struct ONB {
 
 // ---------------------------------------------------------------- PDFs (pdf.rs) ----
 struct Pdf {
-    int kind = 0;  // 0 cosine, 1 reflection
-    ONB onb;          // cosine: about n; reflection: onb_normal
+    int kind = 0;  // 0 cosine, 1 reflection, 2 sphere, 3 Blinn-Phong
+    ONB onb;          // cosine: about n; reflection / Blinn-Phong: onb_normal
     ONB onb_reflected;
     double exponent = 0;
+    Vec3 r_in;        // Blinn-Phong
+    double k_specular = 0;
     double value(const Vec3& d) const {
         if (kind == 0) {  // pdf.rs:30-36
             double c = d.dot(onb.axis[2]);
             return c < 0.0 ? 0.0 : c / PI;
         }
+        if (kind == 2) return 1.0 / (4.0 * PI);  // pdf.rs:228-230
+        if (kind == 3) {  // pdf.rs:177-193
+            double cosine = d.dot(onb.axis[2]);
+            Vec3 random_normal = (-r_in + d).unit();
+            double cosine_specular = std::fmax(random_normal.dot(onb.axis[2]), 0.0);
+            double normal_pdf = (exponent + 1.0) / (2.0 * PI) * lm_pow(cosine_specular, exponent);
+            return std::fmax(cosine / PI, 0.0) * (1.0 - k_specular) +
+                   normal_pdf / (4.0 * (r_in * -1.0).dot(random_normal)) * k_specular;
+        }
         double c = d.dot(onb_reflected.axis[2]);  // pdf.rs:109-116
         double v = c / PI;
         return v < 0.0 ? 0.0 : v;
     }
-    Vec3 generate(FastRng& rng) const {
-        if (kind == 0) return onb.local(random_cosine_direction(rng));  // pdf.rs:39-41
-        for (int i = 0; i < RS_REJECTION_CAP; ++i) {  // pdf.rs:118-134
+    Vec3 lobe(FastRng& rng) const {  // pdf.rs:118-134 / :196-206
+        for (int i = 0; i < RS_REJECTION_CAP; ++i) {
             Vec3 d = onb_reflected.local(random_cosine_direction_exponent(exponent, rng));
             if (d.dot(onb.axis[2]) > 0.0) return d;
         }
         return onb.axis[2];
+    }
+    Vec3 generate(FastRng& rng) const {
+        if (kind == 0) return onb.local(random_cosine_direction(rng));  // pdf.rs:39-41
+        if (kind == 2) return random_unit(rng);                          // pdf.rs:232-234
+        if (kind == 3) {                                                 // pdf.rs:196-211
+            if (rng.gen() < k_specular) return lobe(rng);
+            return onb.local(random_cosine_direction(rng));
+        }
+        return lobe(rng);
+    }
+    static Pdf sphere() { Pdf p; p.kind = 2; return p; }
+    static Pdf blinn_phong(const Vec3& r_in, const Vec3& n, double k, double e) {  // pdf.rs:153-172
+        Pdf p; p.kind = 3; p.r_in = r_in; p.k_specular = k; p.exponent = e;
+        p.onb_reflected = ONB::build_from(reflect_v(r_in, n));
+        p.onb = ONB::build_from(n);
+        return p;
     }
     static Pdf cosine(const Vec3& n) { Pdf p; p.kind = 0; p.onb = ONB::build_from(n); return p; }
     static Pdf reflection(const Vec3& r_in, const Vec3& n, double e) {  // pdf.rs:88-103
@@ -308,13 +367,110 @@ struct AABB {
 };
 
 // ---------------------------------------------------------------- textures ----
+// Rust `as isize` / `as u32` from f64: truncation toward zero, saturating, NaN -> 0
+static inline int64_t as_isize(double x) {
+    if (!(x == x)) return 0;
+    if (x >= 9223372036854775807.0) return INT64_MAX;
+    if (x <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)x;
+}
+static inline uint32_t as_u32(double x) {
+    if (!(x > 0.0)) return 0u;
+    if (x >= 4294967295.0) return 0xffffffffu;
+    return (uint32_t)x;
+}
+
+struct Perlin {  // texture/noise.rs
+    int type = RS_PERLIN_NORMAL, smooth = RS_SMOOTH_HERMITE;
+    bool vector = false;
+    uint32_t point_count = 0, depth = 0;
+    double scale = 1.0;
+    std::vector<double> values;                 // 3 per point (Vector) or 1 (Float)
+    std::vector<uint32_t> perm_x, perm_y, perm_z;
+    double val(size_t i, int c) const { return vector ? values[3 * i + c] : values[i]; }
+    // noise.rs:111-148
+    double noise(const Vec3& p) const {
+        const int64_t mask = (int64_t)point_count - 1;
+        if (smooth == RS_SMOOTH_NONE) {
+            int64_t i = as_isize(4.0 * p.x) & mask, j = as_isize(4.0 * p.y) & mask, k = as_isize(4.0 * p.z) & mask;
+            return val(perm_x[i] ^ perm_y[j] ^ perm_z[k], 0);
+        }
+        int64_t i = as_isize(std::floor(p.x)), j = as_isize(std::floor(p.y)), k = as_isize(std::floor(p.z));
+        double u = p.x - (double)i, v = p.y - (double)j, w = p.z - (double)k;
+        // interpolate (noise.rs:170-207); f64 sums start from 0.0
+        double uu = u, vv = v, ww = w;
+        if (smooth == RS_SMOOTH_HERMITE) {
+            uu = u * u * (3.0 - 2.0 * u);
+            vv = v * v * (3.0 - 2.0 * v);
+            ww = w * w * (3.0 - 2.0 * w);
+        }
+        double si = 0.0;
+        for (int a = 0; a < 2; ++a) {
+            double sj = 0.0;
+            for (int b = 0; b < 2; ++b) {
+                double sk = 0.0;
+                for (int c = 0; c < 2; ++c) {
+                    int64_t xi = (int64_t)((uint64_t)i + (uint64_t)a) & mask;
+                    int64_t yi = (int64_t)((uint64_t)j + (uint64_t)b) & mask;
+                    int64_t zi = (int64_t)((uint64_t)k + (uint64_t)c) & mask;
+                    size_t idx = perm_x[xi] ^ perm_y[yi] ^ perm_z[zi];
+                    double g = vector ? Vec3(val(idx, 0), val(idx, 1), val(idx, 2)).dot(Vec3(u - a, v - b, w - c)) : val(idx, 0);
+                    sk = sk + std::fma((double)a, uu, (double)(1 - a) * (1.0 - uu)) *
+                                  std::fma((double)b, vv, (double)(1 - b) * (1.0 - vv)) *
+                                  std::fma((double)c, ww, (double)(1 - c) * (1.0 - ww)) * g;
+                }
+                sj = sj + sk;
+            }
+            si = si + sj;
+        }
+        return si;
+    }
+    // noise.rs:150-166
+    double turbulence(Vec3 p, uint32_t d) const {
+        double weight = 1.0, acc = 0.0;
+        for (uint32_t n = 0; n < d; ++n) {
+            acc = acc + weight * noise(p);
+            weight *= 0.5;
+            p = Vec3(p.x * 2.0, p.y * 2.0, p.z * 2.0);
+        }
+        return std::fabs(acc);
+    }
+    // noise.rs:187-211 (the factor of Color(1,1,1,1) * value)
+    double value(const Vec3& p) const {
+        if (type == RS_PERLIN_TURBULENCE) return turbulence(p, depth);
+        if (type == RS_PERLIN_MARBLE) return (lm_sin(std::fma(scale, p.z, 10.0 * turbulence(p, depth))) + 1.0) * 0.5;
+        double n = noise(Vec3(scale * p.x, scale * p.y, scale * p.z));
+        if (vector) n = 0.5 * (n + 1.0);
+        return n;
+    }
+};
+
+struct ImageTex {  // texture/image.rs (decoded 8-bit RGB, row 0 = top)
+    uint32_t w = 0, h = 0;
+    std::vector<uint8_t> rgb;
+};
+
 struct Texture {
     int kind = RS_TEX_SOLID;
     Color even, odd;
     double scale = 1;
-    // checker.rs:21-30
-    Color color(double, double, const Vec3& p) const {
+    const Perlin* perlin = nullptr;
+    const ImageTex* image = nullptr;
+    // color.rs:61-65, checker.rs:21-30, noise.rs:187-211, image.rs:34-50
+    Color color(double u, double v, const Vec3& p) const {
         if (kind == RS_TEX_SOLID) return even;
+        if (kind == RS_TEX_PERLIN) {
+            float f = (float)perlin->value(p);
+            return Color(1.0f * f, 1.0f * f, 1.0f * f, 1.0f);
+        }
+        if (kind == RS_TEX_IMAGE) {
+            double vv = 1.0 - v;
+            uint32_t x = as_u32(u * (double)image->w), y = as_u32(vv * (double)image->h);
+            if (x >= image->w) x = image->w - 1;
+            if (y >= image->h) y = image->h - 1;
+            const uint8_t* q = &image->rgb[3 * ((size_t)y * image->w + x)];
+            return Color((float)q[0] / 255.0f, (float)q[1] / 255.0f, (float)q[2] / 255.0f, 1.0f);
+        }
         return lm_sin3_negative(scale * p.x, scale * p.y, scale * p.z) ? odd : even;  // sin sin sin < 0
     }
 };
@@ -345,6 +501,7 @@ struct Material {
     bool glass = false;
     double enter_refractive = 1, outer_refractive = 1;
     double exponent = 0;
+    double k_specular = 0;
     double multiplier = 1;
     const Material* m1 = nullptr;
     const Material* m2 = nullptr;
@@ -424,6 +581,18 @@ struct Material {
             s.has_ray = true; s.ray = r; s.pdf = Pdf::cosine(hit.normal); s.skip_pdf = true;
             return true;
         }
+        case RS_MAT_ISOTROPIC:  // isotropic.rs:25-33
+            s.color = tex.even;
+            s.has_ray = false;
+            s.pdf = Pdf::sphere();
+            s.skip_pdf = false;
+            return true;
+        case RS_MAT_BLINN_PHONG:  // blinn_phong.rs:32-42
+            s.color = tex.color(hit.u, hit.v, hit.point);
+            s.has_ray = false;
+            s.pdf = Pdf::blinn_phong(ray.direction, hit.normal, k_specular, exponent);
+            s.skip_pdf = false;
+            return true;
         case RS_MAT_MIXED:  // mixed_material.rs:43-50; thread_rng().next_u32() -> stream
             if ((double)rng.next_u32() < 4294967295.0 * p1) return m1->scatter(ray, hit, rng, s);
             return m2->scatter(ray, hit, rng, s);
@@ -535,6 +704,10 @@ struct Counters { uint64_t segments = 0; };
 
 struct Hittable {
     virtual ~Hittable() = default;
+    // (u, v) are computed only when the scene has an Image texture, their only reader (commit sets
+    // this on every handle); upstream computes them at every candidate hit (sphere.rs:64-71), which
+    // only makes this CPU baseline faster than the reference, never slower
+    bool uv_on = false;
     virtual Vec3 normal(const Vec3&) const { return Vec3(0, 1, 0); }
     virtual const Material* material() const { return nullptr; }
     virtual void uv(const Vec3&, double& u, double& v) const { u = 0; v = 0; }
@@ -554,7 +727,7 @@ static HitRecord make_hit(const Ray& ray, const Hittable& obj, double t1, double
     h.outside = ray.direction.dot(h.normal) < 0.0;
     if (!h.outside) h.normal = -h.normal;
     h.material = obj.material();
-    obj.uv(h.point, h.u, h.v);
+    if (obj.uv_on) obj.uv(h.point, h.u, h.v);
     h.t1 = t1; h.t2 = t2;
     return h;
 }
@@ -575,8 +748,8 @@ struct Sphere : Hittable {  // sphere.rs
     const Material* material() const override { return mat; }
     void uv(const Vec3& point, double& u, double& v) const override {  // sphere.rs:64-71
         Vec3 p = (point - center).unit();
-        double phi = std::atan2(-p.z, p.x);
-        double theta = std::asin(p.y);
+        double phi = lm_atan2(-p.z, p.x);
+        double theta = lm_asin(p.y);
         u = phi / 2.0 / PI + 0.5;
         v = theta / PI + 0.5;
     }
@@ -850,6 +1023,7 @@ struct TfFacade : Hittable {  // transform/tf_facade.rs
     TfFacade(std::shared_ptr<Hittable> o, TransformStack s) : object(o), stack(std::move(s)) {}
     bool hit(const Ray& rin, double tmin, double tmax, HitRecord& rec) const override {  // :41-55
         Ray r(stack.inverse(rin.origin, 1.0), stack.inverse(rin.direction, 0.0), rin.time);
+        r.key = rin.key;
         if (!object->hit(r, tmin, tmax, rec)) return false;
         rec.point = stack.forward(rec.point, 1.0);
         return true;
@@ -868,6 +1042,38 @@ struct TfFacade : Hittable {  // transform/tf_facade.rs
     }
     bool contains(const Vec3& p) const override { return object->contains(stack.inverse(p, 1.0)); }
     Vec3 random(const Vec3& origin, FastRng& rng) const override { return object->random(stack.inverse(origin, 1.0), rng); }
+};
+
+struct ConstantMedium : Hittable {  // medium/constant.rs
+    std::shared_ptr<Hittable> boundary;
+    const Material* mat;     // Isotropic(color)
+    double neg_inv_density;
+    uint32_t handle = 0;     // this object's handle (medium_uniform)
+    ConstantMedium(std::shared_ptr<Hittable> b, const Material* m, double density)
+        : boundary(std::move(b)), mat(m), neg_inv_density(-1.0 / density) {}
+    bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // :42-84
+        HitRecord rec1, rec2;
+        if (!boundary->hit(ray, -INFINITY, INFINITY, rec1)) return false;
+        if (!boundary->hit(ray, rec1.t1 + 0.0001, INFINITY, rec2)) return false;
+        if (rec1.t1 < tmin) rec1.t1 = tmin;
+        if (rec2.t1 > tmax) rec2.t1 = tmax;
+        if (rec1.t1 >= rec2.t1) return false;
+        if (rec1.t1 < 0.0) rec1.t1 = 0.0;
+        double length_per_unit = ray.direction.length();
+        double distance_inside = (rec2.t1 - rec1.t1) * length_per_unit;
+        double hit_distance = neg_inv_density * lm_log(medium_uniform(ray.key, handle));  // Random::normal().ln()
+        if (hit_distance > distance_inside) return false;
+        double t = rec1.t1 + hit_distance / length_per_unit;
+        rec = HitRecord();
+        rec.point = ray.at(t);
+        rec.normal = Vec3(1.0, 0.0, 0.0);
+        rec.material = mat;
+        rec.t1 = t; rec.t2 = t; rec.u = 0.0; rec.v = 0.0; rec.outside = false;
+        return true;
+    }
+    bool contains(const Vec3&) const override { return false; }  // unimplemented! upstream
+    AABB bbox(double t0, double t1) const override { return boundary->bbox(t0, t1); }
+    Vec3 random(const Vec3&, FastRng&) const override { return Vec3(1.0, 0.0, 0.0); }
 };
 
 // bvh.rs:47-113 (deterministic axis, one object per leaf: see header)
@@ -931,6 +1137,8 @@ struct BVH {
 // ---------------------------------------------------------------- world + camera ----
 struct Scene {
     std::vector<std::unique_ptr<Material>> materials;
+    std::vector<std::unique_ptr<Perlin>> perlins;
+    std::vector<std::unique_ptr<ImageTex>> images;
     std::vector<std::shared_ptr<Hittable>> handles;
     std::vector<uint32_t> world, lights;
     Color bg_lo{0.3f, 0.4f, 0.5f, 1.0f}, bg_hi{0.7f, 0.89f, 1.0f, 1.0f};
@@ -1019,7 +1227,9 @@ static Vec3 ray_color(const Scene& sc, const Ray& ray, uint32_t depth, FastRng& 
     if (depth == 0) return Vec3();
     HitRecord hit;
     cnt.segments++;
-    const bool any = sc.world_hit(ray, 0.0001, INFINITY, hit);
+    Ray keyed = ray;
+    keyed.key = medium_key(rng);  // read only by ConstantMedium::hit
+    const bool any = sc.world_hit(keyed, 0.0001, INFINITY, hit);
     if (g_trace)
         std::fprintf(stderr, "depth %u o (%.17g %.17g %.17g) d (%.17g %.17g %.17g) hit %d t1 %.17g p (%.17g %.17g %.17g) n (%.17g %.17g %.17g) outside %d mat %d\n",
                      depth, ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x, ray.direction.y, ray.direction.z,
@@ -1093,6 +1303,16 @@ int orc_material(orc_scene* s, const rs_material_desc* d, int32_t* id_out) {
     m->tex.even = Color(d->texture.even[0], d->texture.even[1], d->texture.even[2], d->texture.even[3]);
     m->tex.odd = Color(d->texture.odd[0], d->texture.odd[1], d->texture.odd[2], d->texture.odd[3]);
     m->tex.scale = d->texture.scale;
+    if (d->texture.kind == RS_TEX_PERLIN) {
+        if (d->texture.data < 0 || (size_t)d->texture.data >= s->s.perlins.size()) return fail(RS_E_INVALID, "unknown perlin id");
+        m->tex.perlin = s->s.perlins[d->texture.data].get();
+    } else if (d->texture.kind == RS_TEX_IMAGE) {
+        if (d->texture.data < 0 || (size_t)d->texture.data >= s->s.images.size()) return fail(RS_E_INVALID, "unknown image id");
+        m->tex.image = s->s.images[d->texture.data].get();
+    } else if (d->texture.kind != RS_TEX_SOLID && d->texture.kind != RS_TEX_CHECKER) {
+        return fail(RS_E_INVALID, "unknown texture kind");
+    }
+    m->k_specular = d->k_specular;
     m->glass = d->glass != 0;
     m->enter_refractive = 1.0 / d->refractive;  // dielectric.rs:35-41
     m->outer_refractive = d->refractive;
@@ -1106,7 +1326,7 @@ int orc_material(orc_scene* s, const rs_material_desc* d, int32_t* id_out) {
         m->m2 = s->s.mat(d->mix_b);
         if (!m->m1 || !m->m2) return fail(RS_E_INVALID, "mixed material refers to unknown ids");
     }
-    if (d->kind < 0 || d->kind > RS_MAT_MIXED) return fail(RS_E_INVALID, "unknown material kind");
+    if (d->kind < 0 || d->kind > RS_MAT_BLINN_PHONG) return fail(RS_E_INVALID, "unknown material kind");
     m->id = (int)s->s.materials.size();
     *id_out = m->id;
     s->s.materials.push_back(std::move(m));
@@ -1119,6 +1339,44 @@ static int push_handle(orc_scene* s, std::shared_ptr<Hittable> h, uint32_t* out)
     return RS_OK;
 }
 
+int orc_perlin(orc_scene* s, const rs_perlin_desc* d, int32_t* id) {
+    if (!s || !d || !id) return fail(RS_E_INVALID, "null argument");
+    auto p = std::make_unique<Perlin>();
+    const uint32_t n = d->point_count;
+    if (n == 0 || (n & (n - 1)) != 0) return fail(RS_E_INVALID, "point_count must be a power of two");
+    p->type = d->type; p->smooth = d->smooth; p->vector = d->vector != 0; p->point_count = n; p->depth = d->depth;
+    p->scale = d->scale;
+    p->values.assign(d->values, d->values + (size_t)n * (d->vector ? 3 : 1));
+    p->perm_x.assign(d->perm_x, d->perm_x + n);
+    p->perm_y.assign(d->perm_y, d->perm_y + n);
+    p->perm_z.assign(d->perm_z, d->perm_z + n);
+    *id = (int32_t)s->s.perlins.size();
+    s->s.perlins.push_back(std::move(p));
+    return RS_OK;
+}
+int orc_image(orc_scene* s, const uint8_t* rgb, uint32_t w, uint32_t h, int32_t* id) {
+    if (!s || !rgb || !id || !w || !h) return fail(RS_E_INVALID, "bad image");
+    auto im = std::make_unique<ImageTex>();
+    im->w = w; im->h = h;
+    im->rgb.assign(rgb, rgb + (size_t)w * h * 3);
+    *id = (int32_t)s->s.images.size();
+    s->s.images.push_back(std::move(im));
+    return RS_OK;
+}
+int orc_constant_medium(orc_scene* s, uint32_t boundary, const float color[4], double density, uint32_t* out) {
+    if (boundary >= s->s.handles.size()) return fail(RS_E_INVALID, "bad handle");
+    // ConstantMedium::new (constant.rs:29-39) creates its Isotropic(color) material
+    auto m = std::make_unique<Material>();
+    m->kind = RS_MAT_ISOTROPIC;
+    m->tex.kind = RS_TEX_SOLID;
+    m->tex.even = m->tex.odd = Color(color[0], color[1], color[2], color[3]);
+    m->id = (int)s->s.materials.size();
+    const Material* mp = m.get();
+    s->s.materials.push_back(std::move(m));
+    auto med = std::make_shared<ConstantMedium>(s->s.handles[boundary], mp, density);
+    med->handle = (uint32_t)s->s.handles.size();
+    return push_handle(s, med, out);
+}
 int orc_sphere(orc_scene* s, const double c[3], double r, const double speed[3], int32_t mat, uint32_t* out) {
     Vec3 sp = speed ? Vec3(speed[0], speed[1], speed[2]) : Vec3();
     return push_handle(s, std::make_shared<Sphere>(Vec3(c[0], c[1], c[2]), r, sp, s->s.mat(mat)), out);
@@ -1177,6 +1435,13 @@ int orc_set_time_range(orc_scene* s, double t0, double t1) {
     s->s.time0 = t0; s->s.time1 = t1; return RS_OK;
 }
 int orc_commit(orc_scene* s) {
+    bool uv = false;
+    for (const auto& m : s->s.materials) uv = uv || m->tex.kind == RS_TEX_IMAGE;
+    for (auto& h : s->s.handles) {
+        h->uv_on = uv;
+        if (auto* b = dynamic_cast<BoxShape*>(h.get()))
+            for (auto& f : b->faces) f.uv_on = uv;  // the box's records are its faces' (box.rs:125-149)
+    }
     std::vector<std::pair<const Hittable*, AABB>> objs;
     for (uint32_t h : s->s.world) {
         const Hittable* o = s->s.handles[h].get();

@@ -18,6 +18,15 @@ RS_E_NOMEM = -6
 
 RS_TEX_SOLID = 0
 RS_TEX_CHECKER = 1
+RS_TEX_PERLIN = 2
+RS_TEX_IMAGE = 3
+
+RS_PERLIN_NORMAL = 0
+RS_PERLIN_TURBULENCE = 1
+RS_PERLIN_MARBLE = 2
+RS_SMOOTH_NONE = 0
+RS_SMOOTH_LINEAR = 1
+RS_SMOOTH_HERMITE = 2
 
 RS_MAT_LAMBERTIAN = 0
 RS_MAT_METAL = 1
@@ -25,6 +34,8 @@ RS_MAT_DIFFUSE_METAL = 2
 RS_MAT_DIELECTRIC = 3
 RS_MAT_DIFFUSE_LIGHT = 4
 RS_MAT_MIXED = 5
+RS_MAT_ISOTROPIC = 6
+RS_MAT_BLINN_PHONG = 7
 RS_NO_MATERIAL = -1
 
 RS_PLANE_XY = 0
@@ -43,7 +54,7 @@ RS_MODE_WAVEFRONT = 2
 
 
 class rs_texture_desc(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("_pad", C.c_int32), ("even", C.c_float * 4), ("odd", C.c_float * 4),
+    _fields_ = [("kind", C.c_int32), ("data", C.c_int32), ("even", C.c_float * 4), ("odd", C.c_float * 4),
                 ("scale", C.c_double)]
 
 
@@ -51,7 +62,14 @@ class rs_material_desc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("glass", C.c_int32), ("texture", rs_texture_desc), ("refractive", C.c_double),
                 ("exponent", C.c_double), ("multiplier", C.c_double), ("mix_a", C.c_int32), ("mix_b", C.c_int32),
                 ("mix_p", C.c_double), ("phong_factor", C.c_double), ("phong_exponent", C.c_int32),
-                ("_pad", C.c_int32)]
+                ("_pad", C.c_int32), ("k_specular", C.c_double)]
+
+
+class rs_perlin_desc(C.Structure):
+    _fields_ = [("point_count", C.c_uint32), ("vector", C.c_int32), ("smooth", C.c_int32), ("type", C.c_int32),
+                ("depth", C.c_uint32), ("_pad", C.c_int32), ("scale", C.c_double),
+                ("values", C.POINTER(C.c_double)), ("perm_x", C.POINTER(C.c_uint32)),
+                ("perm_y", C.POINTER(C.c_uint32)), ("perm_z", C.POINTER(C.c_uint32))]
 
 
 class rs_transform(C.Structure):
@@ -105,6 +123,9 @@ SCENE_SIGNATURES = {
     "lights_add": (C.c_int, [VP, C.c_uint32]),
     "set_background": (C.c_int, [VP, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "set_time_range": (C.c_int, [VP, C.c_double, C.c_double]),
+    "perlin": (C.c_int, [VP, C.POINTER(rs_perlin_desc), I32P]),
+    "image": (C.c_int, [VP, C.c_void_p, C.c_uint32, C.c_uint32, I32P]),
+    "constant_medium": (C.c_int, [VP, C.c_uint32, C.POINTER(C.c_float), C.c_double, U32P]),
 }
 
 _LIB = None
@@ -132,6 +153,8 @@ def load() -> C.CDLL:
     lib.rs_device_count.argtypes = [C.POINTER(C.c_int)]
     lib.rs_stream_key.restype = C.c_uint64
     lib.rs_stream_key.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]
+    lib.rs_medium_uniform.restype = C.c_double
+    lib.rs_medium_uniform.argtypes = [C.POINTER(C.c_uint32), C.c_uint32]
     lib.rs_scene_create.argtypes = [C.POINTER(VP)]
     lib.rs_scene_destroy.argtypes = [VP]
     lib.rs_scene_commit.argtypes = [VP]
@@ -152,7 +175,7 @@ def load() -> C.CDLL:
     for fn in ("rs_probe_world_hit", "rs_scene_create", "rs_scene_destroy", "rs_scene_commit", "rs_render", "rs_render_device",
                "rs_device_count"):
         getattr(lib, fn).restype = C.c_int
-    if lib.rs_abi_version() != 1:
+    if lib.rs_abi_version() != 2:
         raise RuntimeError("libraysnail_hip.so ABI mismatch")
     _LIB = lib
     return lib
@@ -160,9 +183,9 @@ def load() -> C.CDLL:
 
 # every symbol include/raysnail_hip.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
-    "rs_abi_version", "rs_last_error", "rs_device_count", "rs_stream_key", "rs_scene_create", "rs_scene_destroy",
-    "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
-    "rs_difference", "rs_transformed", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
+    "rs_abi_version", "rs_last_error", "rs_device_count", "rs_stream_key", "rs_medium_uniform", "rs_scene_create",
+    "rs_scene_destroy", "rs_perlin", "rs_image", "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
+    "rs_difference", "rs_transformed", "rs_constant_medium", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
     "rs_scene_commit", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
     "rs_probe_world_hit", "rs_probe_samples",
 ]

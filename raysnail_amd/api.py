@@ -56,9 +56,60 @@ class Checker:
     scale: float
 
 
-def _tex_desc(t) -> A.rs_texture_desc:
+class SmoothType:                    # src/texture/noise.rs:4-9
+    None_ = A.RS_SMOOTH_NONE
+    LinearInterpolate = A.RS_SMOOTH_LINEAR
+    HermitianCubic = A.RS_SMOOTH_HERMITE
+
+
+class Perlin:
+    """src/texture/noise.rs. Perlin::new(point_count, vector, rng) draws its tables from a FastRng the
+    reference seeds from the OS; here the FastRng seed is explicit (tables built by the C++ host
+    layer: Vec3::random_unit / gen values, rand 0.8 shuffles)."""
+
+    def __init__(self, point_count: int, vector: bool, rng_seed: int):
+        from . import host_lib
+        self.point_count, self.vector = int(point_count), bool(vector)
+        self.values, self.perms = host_lib.perlin_tables(int(rng_seed), self.point_count, self.vector)
+        self._scale, self._smooth, self._type, self._depth = 1.0, SmoothType.HermitianCubic, A.RS_PERLIN_NORMAL, 0
+
+    def scale(self, s):
+        self._scale = float(s); return self
+
+    def smooth(self, t):
+        self._smooth = int(t); return self
+
+    def turbulence(self, depth: int):
+        self._type, self._depth = A.RS_PERLIN_TURBULENCE, int(depth); return self
+
+    def marble(self, depth: int):
+        self._type, self._depth = A.RS_PERLIN_MARBLE, int(depth); return self
+
+
+class Image:
+    """src/texture/image.rs: decoded 8-bit RGB pixels, row 0 = top."""
+
+    def __init__(self, rgb: np.ndarray):
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+        assert rgb.ndim == 3 and rgb.shape[2] == 3, "H x W x 3 uint8 expected"
+        self.rgb = rgb
+
+    @staticmethod
+    def new(path: str) -> "Image":
+        """Image::new (image.rs:24-31): PNG decode by the C++ host layer."""
+        from . import host_lib
+        return Image(host_lib.png_load(path))
+
+
+def _tex_desc(t, data: int = 0) -> A.rs_texture_desc:
     d = A.rs_texture_desc()
-    if isinstance(t, Color):
+    d.data = data
+    if isinstance(t, (Perlin, Image)):
+        d.kind = A.RS_TEX_PERLIN if isinstance(t, Perlin) else A.RS_TEX_IMAGE
+        d.even[:] = [1.0, 1.0, 1.0, 1.0]
+        d.odd[:] = [1.0, 1.0, 1.0, 1.0]
+        d.scale = 1.0
+    elif isinstance(t, Color):
         d.kind = A.RS_TEX_SOLID
         d.even[:] = [t.r, t.g, t.b, t.a]
         d.odd[:] = [t.r, t.g, t.b, t.a]
@@ -69,7 +120,7 @@ def _tex_desc(t) -> A.rs_texture_desc:
         d.odd[:] = [t.odd.r, t.odd.g, t.odd.b, t.odd.a]
         d.scale = float(t.scale)
     else:
-        raise TypeError(f"unsupported texture {type(t).__name__} (Image/Perlin are outside the GPU path)")
+        raise TypeError(f"unsupported texture {type(t).__name__}")
     return d
 
 
@@ -127,6 +178,17 @@ class DiffuseLight(Material):        # src/material/light.rs
     def multiplier(self, m: float):
         self.mult = float(m)
         return self
+
+
+class Isotropic(Material):           # src/material/isotropic.rs
+    def __init__(self, color: Color):
+        self.color, self.settings = color, CommonMaterialSettings()
+
+
+class BlinnPhong(Material):          # src/material/blinn_phong.rs
+    def __init__(self, k_specular: float, exponent: float, texture):
+        self.k_specular, self.exponent, self.texture = float(k_specular), float(exponent), texture
+        self.settings = CommonMaterialSettings()
 
 
 class MixedMaterial(Material):       # src/material/mixed_material.rs
@@ -197,6 +259,28 @@ class TriangleMesh(Hittable):        # src/hittable/geometry/triangle_mesh.rs (T
         self.positions = np.ascontiguousarray(positions, dtype=np.float64).reshape(-1, 9)
         self.normals = None if normals is None else np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 9)
         self.material = material
+
+    @staticmethod
+    def load(filename: str, scale: float, offset, rotation_angle: float, axis: int,
+             material: Optional[Material]) -> "TriangleMesh":
+        """TriangleMesh::load (triangle_mesh.rs:166-276): OBJ through the C++ host layer's
+        tobj-compatible reader (single_index, triangulate)."""
+        from . import host_lib
+        pos, nrm = host_lib.obj_load(filename, scale, offset, rotation_angle, axis)
+        return TriangleMesh(pos, nrm, material)
+
+
+class ConstantMedium(Hittable):      # src/hittable/medium/constant.rs (material Isotropic(color))
+    def __init__(self, boundary: Hittable, color: Color, density: float):
+        self.boundary, self.color, self.density = boundary, color, float(density)
+
+
+class BVH(Hittable):
+    """A BVH / HittableList used as one object (bvh.rs, list.rs): the device scene has one BVH over
+    every object, so the group exports its members (a TfFacade of a group transforms each member)."""
+
+    def __init__(self, objects, time_limit=(0.0, 0.0)):
+        self.objects = list(objects.objects if isinstance(objects, HittableList) else objects)
 
 
 class Intersection(Hittable):        # src/hittable/csg/intersection.rs
@@ -295,9 +379,31 @@ def realize(world: World, lib, handle, prefix: str = "rs_") -> None:
     """Replay the world description into a backend scene (libraysnail_hip or the test oracle)."""
     mat_ids = {}
     obj_ids = {}
+    tex_ids = {}
 
     def call(name, *args):
         _check(lib, getattr(lib, prefix + name)(handle, *args), prefix)
+
+    def tex(t) -> A.rs_texture_desc:
+        if not isinstance(t, (Perlin, Image)):
+            return _tex_desc(t)
+        if id(t) not in tex_ids:
+            out = C.c_int32()
+            if isinstance(t, Perlin):
+                pd = A.rs_perlin_desc()
+                pd.point_count, pd.vector, pd.smooth, pd.type = t.point_count, int(t.vector), t._smooth, t._type
+                pd.depth, pd.scale = t._depth, t._scale
+                pd.values = t.values.ctypes.data_as(C.POINTER(C.c_double))
+                n = t.point_count
+                pd.perm_x = t.perms[:n].ctypes.data_as(C.POINTER(C.c_uint32))
+                pd.perm_y = t.perms[n:2 * n].ctypes.data_as(C.POINTER(C.c_uint32))
+                pd.perm_z = t.perms[2 * n:].ctypes.data_as(C.POINTER(C.c_uint32))
+                call("perlin", C.byref(pd), C.byref(out))
+            else:
+                h, w = t.rgb.shape[:2]
+                call("image", t.rgb.ctypes.data_as(C.c_void_p), w, h, C.byref(out))
+            tex_ids[id(t)] = out.value
+        return _tex_desc(t, tex_ids[id(t)])
 
     def mat_id(m: Optional[Material]) -> int:
         if m is None:
@@ -312,22 +418,34 @@ def realize(world: World, lib, handle, prefix: str = "rs_") -> None:
             d.texture = _tex_desc(Color(0, 0, 0))
         else:
             if isinstance(m, Lambertian):
-                d.kind, d.texture = A.RS_MAT_LAMBERTIAN, _tex_desc(m.texture)
+                d.kind, d.texture = A.RS_MAT_LAMBERTIAN, tex(m.texture)
             elif isinstance(m, Metal):
-                d.kind, d.texture = A.RS_MAT_METAL, _tex_desc(m.texture)
+                d.kind, d.texture = A.RS_MAT_METAL, tex(m.texture)
             elif isinstance(m, DiffuseMetal):
-                d.kind, d.texture, d.exponent = A.RS_MAT_DIFFUSE_METAL, _tex_desc(m.texture), m.exponent
+                d.kind, d.texture, d.exponent = A.RS_MAT_DIFFUSE_METAL, tex(m.texture), m.exponent
             elif isinstance(m, Dielectric):
                 d.kind, d.texture, d.refractive, d.glass = A.RS_MAT_DIELECTRIC, _tex_desc(m.color), m.refractive, int(m.glass)
             elif isinstance(m, DiffuseLight):
-                d.kind, d.texture, d.multiplier = A.RS_MAT_DIFFUSE_LIGHT, _tex_desc(m.texture), m.mult
+                d.kind, d.texture, d.multiplier = A.RS_MAT_DIFFUSE_LIGHT, tex(m.texture), m.mult
+            elif isinstance(m, Isotropic):
+                d.kind, d.texture = A.RS_MAT_ISOTROPIC, _tex_desc(m.color)
+            elif isinstance(m, BlinnPhong):
+                d.kind, d.texture = A.RS_MAT_BLINN_PHONG, tex(m.texture)
+                d.k_specular, d.exponent = m.k_specular, m.exponent
             else:
-                raise TypeError(f"unsupported material {type(m).__name__} (Isotropic/BlinnPhong are outside the GPU path)")
+                raise TypeError(f"unsupported material {type(m).__name__}")
             d.phong_factor, d.phong_exponent = m.settings.phong_factor, int(m.settings.phong_exponent)
         out = C.c_int32()
         call("material", C.byref(d), C.byref(out))
         mat_ids[id(m)] = out.value
         return out.value
+
+    def single(h):
+        if isinstance(h, list):
+            if len(h) != 1:
+                raise RaysnailError(A.RS_E_UNSUPPORTED, "operand must be a single object")
+            return h[0]
+        return h
 
     def obj_id(o: Hittable) -> int:
         if id(o) in obj_ids:
@@ -351,17 +469,35 @@ def realize(world: World, lib, handle, prefix: str = "rs_") -> None:
             obj_ids[id(o)] = list(range(out.value, out.value + pos.shape[0]))
             return obj_ids[id(o)]
         elif isinstance(o, Intersection):
-            a, b = obj_id(o.o1), obj_id(o.o2)
+            a, b = single(obj_id(o.o1)), single(obj_id(o.o2))
             call("intersection", a, b, mat_id(o.material), C.byref(out))
         elif isinstance(o, Difference):
-            a, b = obj_id(o.plus), obj_id(o.minus)
+            a, b = single(obj_id(o.plus)), single(obj_id(o.minus))
             call("difference", a, b, mat_id(o.material), C.byref(out))
+        elif isinstance(o, ConstantMedium):
+            b = single(obj_id(o.boundary))
+            c = o.color
+            call("constant_medium", b, (C.c_float * 4)(c.r, c.g, c.b, c.a), o.density, C.byref(out))
+        elif isinstance(o, BVH):
+            hs = []
+            for m in o.objects:
+                h = obj_id(m)
+                hs.extend(h if isinstance(h, list) else [h])
+            obj_ids[id(o)] = hs
+            return hs
         elif isinstance(o, TfFacade):
             child = obj_id(o.obj)
             arr = (A.rs_transform * max(1, len(o.stack)))()
             for i, t in enumerate(o.stack.stack):
                 arr[i].kind = t.kind
                 arr[i].v[:] = list(t.v)
+            if isinstance(child, list):  # a transformed mesh / group: each member transformed
+                hs = []
+                for c in child:
+                    call("transformed", c, arr, len(o.stack), C.byref(out))
+                    hs.append(out.value)
+                obj_ids[id(o)] = hs
+                return hs
             call("transformed", child, arr, len(o.stack), C.byref(out))
         else:
             raise TypeError(f"unsupported hittable {type(o).__name__}")

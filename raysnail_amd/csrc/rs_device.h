@@ -41,7 +41,8 @@ __device__ __forceinline__ V3 ld3(const double* p) { return v3(p[0], p[1], p[2])
 // vec3.rs:171-173 / material/mod.rs:75-81: d - n * (2 * d.n)
 __device__ __forceinline__ V3 reflect_v(V3 d, V3 n) { return d - n * (2.0 * dot(d, n)); }
 
-struct Ray { V3 o, d; double time; };
+// key: the medium key of the segment (rs_medium_uniform); only read when the scene has media
+struct Ray { V3 o, d; double time; uint64_t key; };
 __device__ __forceinline__ V3 ray_at(const Ray& r, double t) {
     return v3(fma(r.d.x, t, r.o.x), fma(r.d.y, t, r.o.y), fma(r.d.z, t, r.o.z));
 }
@@ -82,12 +83,21 @@ struct Rng {
         return (double)((hi << 32) | lo) * 0x1p-64;
     }
     __device__ __forceinline__ double range(double a, double b) { return a + gen() * (b - a); }
+    // the segment's medium key: a hash of the state, not a draw (the stream is not advanced)
+    __device__ __forceinline__ uint64_t medium_key() const {
+        return splitmix64((((uint64_t)y << 32) | x) ^ splitmix64(((uint64_t)w << 32) | z));
+    }
 };
+// ConstantMedium's Random::normal() (constant.rs:63) for medium handle h: uniform in [0, 1]
+__device__ __forceinline__ double medium_uniform(uint64_t key, int h) {
+    return (double)splitmix64(key ^ splitmix64(0x6d656469756d2121ULL + (uint64_t)(uint32_t)h)) * 0x1p-64;
+}
 
 // ------------------------------------------------------------------ hit record ----
 struct Hit {
     V3 p, n;
     double t1, t2;
+    double u, v;   // computed only when the scene reads them (DScene::uv); 0 otherwise
     int32_t mat;
     int32_t outside;
 };
@@ -99,6 +109,7 @@ __device__ __forceinline__ bool in_range(double t, double a, double b) { return 
 __device__ __forceinline__ void finish_rec(Hit& h, const Ray& r, double t1, double t2, V3 nrm, int32_t mat) {
     h.p = ray_at(r, t1);
     h.t1 = t1; h.t2 = t2; h.mat = mat;
+    h.u = 0.0; h.v = 0.0;
     bool outside = dot(r.d, nrm) < 0.0;
     h.n = outside ? nrm : -nrm;
     h.outside = outside;
@@ -123,17 +134,29 @@ __device__ __forceinline__ bool sphere_t(const DSphere& s, const Ray& r, double 
 }
 __device__ __forceinline__ V3 sphere_normal(const DSphere& s, V3 p) { return vdiv(p - ld3(s.c), s.r); }
 
-__device__ __forceinline__ bool sphere_hit(const DSphere& s, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h) {
+// sphere.rs:64-71 (static center; correctly rounded atan2 / asin, rs_crmath.h)
+// (out of line: only image-textured scenes call it; keeps the hot kernels' register budget)
+__device__ __noinline__ void sphere_uv(const DSphere& s, V3 point, double& u, double& v) {
+    const V3 p = unit(point - ld3(s.c));
+    const double phi = rs_cr::atan2_cr(-p.z, p.x);
+    const double theta = rs_cr::asin_cr(p.y);
+    u = phi / 2.0 / RS_PI + 0.5;
+    v = theta / RS_PI + 0.5;
+}
+
+__device__ __forceinline__ bool sphere_hit(const DSphere& s, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h,
+                                           int uv = 0) {
     double t, t2;
     if (!sphere_t(s, r, tmin, tmax, t, t2)) return false;
     V3 p = ray_at(r, t);
     finish_rec(h, r, t, t2, sphere_normal(s, p), mat);
+    if (uv) sphere_uv(s, h.p, h.u, h.v);
     return true;
 }
 
 // rect.rs:101-120
 __device__ __forceinline__ bool rect_hit_raw(int ax0, int ax1, int ax2, double k, double a0, double a1, double b0, double b1,
-                                             int32_t mat, const Ray& r, double tmin, double tmax, Hit& h) {
+                                             int32_t mat, const Ray& r, double tmin, double tmax, Hit& h, int uv = 0) {
     double t1 = (k - comp(r.o, ax2)) / comp(r.d, ax2);
     if (!in_range(t1, tmin, tmax)) return false;
     double a = fma(t1, comp(r.d, ax0), comp(r.o, ax0));
@@ -142,11 +165,12 @@ __device__ __forceinline__ bool rect_hit_raw(int ax0, int ax1, int ax2, double k
     if (b < b0 || b > b1) return false;
     V3 n = v3(ax2 == 0 ? 1.0 : 0.0, ax2 == 1 ? 1.0 : 0.0, ax2 == 2 ? 1.0 : 0.0);
     finish_rec(h, r, t1, RS_FMAX, n, mat);
+    if (uv) { h.u = (a - a0) / (a1 - a0); h.v = (b - b0) / (b1 - b0); }  // rect.rs:94-99 (a_len, b_len)
     return true;
 }
 
 // box.rs:125-149; faces in the order built by box.rs:55-105
-__device__ bool box_hit(const DBox& b, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h) {
+__device__ bool box_hit(const DBox& b, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h, int uv = 0) {
     Hit h0, h1;  // the first two face hits in face order (two named records: no scratch array)
     int n = 0;
 #pragma unroll
@@ -157,7 +181,7 @@ __device__ bool box_hit(const DBox& b, int32_t mat, const Ray& r, double tmin, d
         else            { ax0 = 0; ax1 = 2; ax2 = 1; k = f == 4 ? b.mn[1] : b.mx[1]; a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[2]; b1 = b.mx[2]; }
         if (n < 2) {
             Hit t;
-            if (rect_hit_raw(ax0, ax1, ax2, k, a0, a1, b0, b1, mat, r, tmin, tmax, t)) {
+            if (rect_hit_raw(ax0, ax1, ax2, k, a0, a1, b0, b1, mat, r, tmin, tmax, t, uv)) {
                 if (n == 0) h0 = t; else h1 = t;
                 ++n;
             }
@@ -262,6 +286,7 @@ __device__ bool tri_hit(const DTri& T, int32_t mat, const Ray& r, double tmin, d
     V3 n = ld3(T.n0) * (1.0 - beta - gamma) + ld3(T.n1) * beta + ld3(T.n2) * gamma;
     h.p = ray_at(r, t);
     h.n = n; h.t1 = t; h.t2 = RS_FMAX; h.mat = mat; h.outside = 1;   // with_normal
+    h.u = 0.0; h.v = 0.0;                                                // Triangle::uv (:80-82)
     return true;
 }
 
@@ -282,37 +307,39 @@ __device__ __forceinline__ V3 tf_inverse(const DScene& S, const DXform& X, int n
 }
 
 // ------------------------------------------------------------------ objects (nested) ----
-template <int L> struct Obj;
+// Obj<L, R>: nested-object dispatch L levels deep; R = 1 in the rich scene mode (ConstantMedium,
+// records with (u, v)), 0 elsewhere, so the common kernels carry none of that code.
+template <int L, int R> struct Obj;
 
-template <> struct Obj<-1> {
+template <int R> struct Obj<-1, R> {
     static __device__ bool hit(const DScene&, int, const Ray&, double, double, Hit&) { return false; }
     static __device__ bool contains(const DScene&, int, V3) { return false; }
     static __device__ V3 random(const DScene&, int, V3, Rng&) { return v3(1.0, 0.0, 0.0); }
 };
 
-template <int L> struct Obj {
+template <int L, int R> struct Obj {
     static __device__ bool hit(const DScene& S, int pi, const Ray& r, double tmin, double tmax, Hit& h) {
         const DPrim P = S.prims[pi];
         switch (P.kind) {
-        case PK_SPHERE: return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, tmax, h);
+        case PK_SPHERE: return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         case PK_RECT: {
-            const DRect& R = S.rects[P.idx];
-            return rect_hit_raw(R.ax0, R.ax1, R.ax2, R.k, R.a0, R.a1, R.b0, R.b1, P.mat, r, tmin, tmax, h);
+            const DRect& Q = S.rects[P.idx];
+            return rect_hit_raw(Q.ax0, Q.ax1, Q.ax2, Q.k, Q.a0, Q.a1, Q.b0, Q.b1, P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         }
-        case PK_BOX: return box_hit(S.boxes[P.idx], P.mat, r, tmin, tmax, h);
+        case PK_BOX: return box_hit(S.boxes[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         case PK_QUADRIC: return quadric_hit(S.quadrics[P.idx], P.mat, r, tmin, tmax, h);
         case PK_TRIANGLE: return tri_hit(S.tris[P.idx], P.mat, r, tmin, tmax, h);
         case PK_AND: {  // csg/intersection.rs:58-100
             const DCsg C = S.csgs[P.idx];
             Hit h1, h2;
-            bool ok1 = Obj<L - 1>::hit(S, C.a, r, tmin, tmax, h1);
-            bool ok2 = Obj<L - 1>::hit(S, C.b, r, tmin, tmax, h2);
+            bool ok1 = Obj<L - 1, R>::hit(S, C.a, r, tmin, tmax, h1);
+            bool ok2 = Obj<L - 1, R>::hit(S, C.b, r, tmin, tmax, h2);
             if (!(ok1 && ok2)) return false;
             const bool first1 = h1.t1 < h2.t1;
             const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
             const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
-            if (Obj<L - 1>::contains(S, o1, p0)) { h = first1 ? h1 : h2; }
-            else if (Obj<L - 1>::contains(S, o0, p1)) { h = first1 ? h2 : h1; }
+            if (Obj<L - 1, R>::contains(S, o1, p0)) { h = first1 ? h1 : h2; }
+            else if (Obj<L - 1, R>::contains(S, o0, p1)) { h = first1 ? h2 : h1; }
             else return false;
             if (h.mat < 0) h.mat = P.mat;  // set_material_if_none (hit.rs:69-78)
             return true;
@@ -320,12 +347,12 @@ template <int L> struct Obj {
         case PK_SUB: {  // csg/difference.rs:57-106
             const DCsg C = S.csgs[P.idx];
             Hit hp, hm;
-            bool okp = Obj<L - 1>::hit(S, C.a, r, tmin, tmax, hp);
-            bool okm = Obj<L - 1>::hit(S, C.b, r, tmin, tmax, hm);
+            bool okp = Obj<L - 1, R>::hit(S, C.a, r, tmin, tmax, hp);
+            bool okm = Obj<L - 1, R>::hit(S, C.b, r, tmin, tmax, hm);
             if (!okp) return false;
             if (!okm) { h = hp; return true; }
             if (hp.t1 < hm.t1) {
-                if (Obj<L - 1>::contains(S, C.b, hp.p)) return false;
+                if (Obj<L - 1, R>::contains(S, C.b, hp.p)) return false;
                 h = hp;
             } else if (hm.t2 < hp.t1) {
                 h = hp;
@@ -333,6 +360,7 @@ template <int L> struct Obj {
                 V3 p = ray_at(r, hm.t2);
                 V3 n = shape_normal(S, C.b, p);
                 h.p = p; h.n = -n; h.mat = S.prims[C.b].mat; h.t1 = hm.t2; h.t2 = hp.t2; h.outside = 1;
+                h.u = 0.0; h.v = 0.0;
             } else {
                 return false;
             }
@@ -345,8 +373,30 @@ template <int L> struct Obj {
             rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
             rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
             rr.time = r.time;
-            if (!Obj<L - 1>::hit(S, X.child, rr, tmin, tmax, h)) return false;
+            rr.key = r.key;
+            if (!Obj<L - 1, R>::hit(S, X.child, rr, tmin, tmax, h)) return false;
             h.p = tf_forward(S, X, P.aux, h.p, 1.0);
+            return true;
+        }
+        case PK_MEDIUM: {  // medium/constant.rs:42-84
+            if (!R) return false;  // media exist only in the rich scene mode
+            const DMedium M = S.media[P.idx];
+            Hit h1, h2;
+            if (!Obj<L - 1, R>::hit(S, M.boundary, r, -RS_INF, RS_INF, h1)) return false;
+            if (!Obj<L - 1, R>::hit(S, M.boundary, r, h1.t1 + 0.0001, RS_INF, h2)) return false;
+            double t1 = h1.t1, t2 = h2.t1;
+            if (t1 < tmin) t1 = tmin;
+            if (t2 > tmax) t2 = tmax;
+            if (t1 >= t2) return false;
+            if (t1 < 0.0) t1 = 0.0;
+            const double length_per_unit = sqrt(len2(r.d));
+            const double distance_inside = (t2 - t1) * length_per_unit;
+            const double hit_distance = M.neg_inv_density * rs_cr::log_cr(medium_uniform(r.key, pi));
+            if (hit_distance > distance_inside) return false;
+            const double th = t1 + hit_distance / length_per_unit;
+            h.p = ray_at(r, th);
+            h.n = v3(1.0, 0.0, 0.0);
+            h.mat = M.mat; h.t1 = th; h.t2 = th; h.u = 0.0; h.v = 0.0; h.outside = 0;
             return true;
         }
         }
@@ -363,13 +413,13 @@ template <int L> struct Obj {
         }
         case PK_BOX: return box_contains(S.boxes[P.idx], p);
         case PK_QUADRIC: return quadric_contains(S.quadrics[P.idx], p);
-        case PK_AND: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1>::contains(S, C.a, p) && Obj<L - 1>::contains(S, C.b, p); }
-        case PK_SUB: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1>::contains(S, C.a, p) && !Obj<L - 1>::contains(S, C.b, p); }
+        case PK_AND: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1, R>::contains(S, C.a, p) && Obj<L - 1, R>::contains(S, C.b, p); }
+        case PK_SUB: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1, R>::contains(S, C.a, p) && !Obj<L - 1, R>::contains(S, C.b, p); }
         case PK_XFORM: {
             const DXform X = S.xforms[P.idx];
-            return Obj<L - 1>::contains(S, X.child, tf_inverse(S, X, P.aux, p, 1.0));
+            return Obj<L - 1, R>::contains(S, X.child, tf_inverse(S, X, P.aux, p, 1.0));
         }
-        default: return false;  // AARect / Triangle: false
+        default: return false;  // AARect / Triangle: false; ConstantMedium: unimplemented! upstream (constant.rs:86-91)
         }
     }
 
@@ -379,21 +429,21 @@ template <int L> struct Obj {
         switch (P.kind) {
         case PK_SPHERE: return sphere_random(S.spheres[P.idx], origin, rng);
         case PK_RECT: {  // rect.rs:141-153 (xz only upstream; returns origin - point)
-            const DRect& R = S.rects[P.idx];
-            V3 root = v3(0.0, R.k, 0.0);
-            root.x = rng.range(R.a0, R.a1);
-            root.z = rng.range(R.b0, R.b1);
+            const DRect& Q = S.rects[P.idx];
+            V3 root = v3(0.0, Q.k, 0.0);
+            root.x = rng.range(Q.a0, Q.a1);
+            root.z = rng.range(Q.b0, Q.b1);
             return origin - root;
         }
         case PK_QUADRIC: return -origin;                                   // quadric.rs:202-205
         case PK_TRIANGLE: return origin - ld3(S.tris[P.idx].p0);          // triangle_mesh.rs:137-139
-        case PK_AND: return Obj<L - 1>::random(S, S.csgs[P.idx].a, origin, rng);
-        case PK_SUB: return Obj<L - 1>::random(S, S.csgs[P.idx].a, origin, rng);
+        case PK_AND: return Obj<L - 1, R>::random(S, S.csgs[P.idx].a, origin, rng);
+        case PK_SUB: return Obj<L - 1, R>::random(S, S.csgs[P.idx].a, origin, rng);
         case PK_XFORM: {
             const DXform X = S.xforms[P.idx];
-            return Obj<L - 1>::random(S, X.child, tf_inverse(S, X, P.aux, origin, 1.0), rng);
+            return Obj<L - 1, R>::random(S, X.child, tf_inverse(S, X, P.aux, origin, 1.0), rng);
         }
-        default: return v3(1.0, 0.0, 0.0);  // Box / BVH
+        default: return v3(1.0, 0.0, 0.0);  // Box / BVH / ConstantMedium (constant.rs:97-99)
         }
     }
 
@@ -426,8 +476,8 @@ __device__ __forceinline__ V3 onb_local(const Onb& o, V3 a) {  // onb.rs:14-24
               o.u.z * a.x + o.v.z * a.y + o.w.z * a.z);
 }
 
-template <int L>
-__device__ V3 Obj<L>::sphere_random(const DSphere& s, V3 origin, Rng& rng) {
+template <int L, int R>
+__device__ V3 Obj<L, R>::sphere_random(const DSphere& s, V3 origin, Rng& rng) {
     V3 c = ld3(s.c);
     Onb uvw = onb_from(c - origin);
     for (int i = 0; i < RS_REJECTION_CAP; ++i) {
@@ -460,30 +510,166 @@ __device__ __forceinline__ V3 random_cosine_direction_exponent(double e, Rng& rn
     return v3(cp * st, sp * st, r2);
 }
 
-// CosinePdf (pdf.rs:20-49) / ReflectionPdf (pdf.rs:86-141)
-struct Pdf {
-    int kind;      // 0 cosine, 1 reflection
-    Onb n;         // cosine: about normal; reflection: onb_normal
-    Onb refl;      // reflection: onb_reflected
-    double exponent;
-};
-__device__ __forceinline__ double pdf_value(const Pdf& p, V3 d) {
-    if (p.kind == 0) { double c = dot(d, p.n.w); return c < 0.0 ? 0.0 : c / RS_PI; }
-    double v = dot(d, p.refl.w) / RS_PI;
-    return v < 0.0 ? 0.0 : v;
+// vec3.rs:91-96
+__device__ __forceinline__ V3 random_unit(Rng& rng) {
+    const double a = rng.range(0.0, 2.0 * RS_PI);
+    const double z = rng.range(-1.0, 1.0);
+    const double r = sqrt(1.0 - z * z);
+    double sa, ca;
+    rs_cr::sincos_cr(a, &sa, &ca);
+    return v3(r * ca, r * sa, z);
 }
-__device__ __forceinline__ V3 pdf_generate(const Pdf& p, Rng& rng) {
-    if (p.kind == 0) return onb_local(p.n, random_cosine_direction(rng));
+
+// CosinePdf (pdf.rs:20-49) / ReflectionPdf (pdf.rs:86-141) / SpherePdf (pdf.rs:215-238) /
+// BlinnPhongPdf (pdf.rs:144-212)
+enum PdfKind { kPdfCosine = 0, kPdfReflection = 1, kPdfSphere = 2, kPdfBlinnPhong = 3 };
+struct Pdf {
+    int kind;      // PdfKind
+    Onb n;         // cosine: about normal; reflection / Blinn-Phong: onb_normal
+    Onb refl;      // reflection / Blinn-Phong: onb_reflected
+    double exponent;
+    V3 rin;        // Blinn-Phong: r_in_direction
+    double k;      // Blinn-Phong: k_specular
+};
+// the Phong lobe about onb_reflected, rejected until it leaves the surface (pdf.rs:118-134, :196-206)
+__device__ __forceinline__ V3 phong_lobe(const Pdf& p, Rng& rng) {
     for (int i = 0; i < RS_REJECTION_CAP; ++i) {
         V3 d = onb_local(p.refl, random_cosine_direction_exponent(p.exponent, rng));
         if (dot(d, p.n.w) > 0.0) return d;
     }
     return p.n.w;
 }
+__device__ __forceinline__ double pdf_value(const Pdf& p, V3 d) {
+    if (p.kind == kPdfCosine) { double c = dot(d, p.n.w); return c < 0.0 ? 0.0 : c / RS_PI; }
+    if (p.kind == kPdfSphere) return 1.0 / (4.0 * RS_PI);
+    if (p.kind == kPdfBlinnPhong) {  // pdf.rs:177-193
+        const double cosine = dot(d, p.n.w);
+        const V3 random_normal = unit(-p.rin + d);
+        const double cosine_specular = fmax(dot(random_normal, p.n.w), 0.0);
+        const double normal_pdf = (p.exponent + 1.0) / (2.0 * RS_PI) * rs_cr::pow_cr(cosine_specular, p.exponent);
+        return fmax(cosine / RS_PI, 0.0) * (1.0 - p.k) + normal_pdf / (4.0 * dot(p.rin * -1.0, random_normal)) * p.k;
+    }
+    double v = dot(d, p.refl.w) / RS_PI;
+    return v < 0.0 ? 0.0 : v;
+}
+__device__ __forceinline__ V3 pdf_generate(const Pdf& p, Rng& rng) {
+    if (p.kind == kPdfCosine) return onb_local(p.n, random_cosine_direction(rng));
+    if (p.kind == kPdfSphere) return random_unit(rng);
+    if (p.kind == kPdfBlinnPhong) {  // pdf.rs:196-211
+        if (rng.gen() < p.k) return phong_lobe(p, rng);
+        return onb_local(p.n, random_cosine_direction(rng));
+    }
+    return phong_lobe(p, rng);
+}
 
-// ------------------------------------------------------------------ materials ----
-// texture eval: Color (color.rs:61-65) / Checker (checker.rs:21-30)
-__device__ __forceinline__ void tex_color(const DMaterial& m, V3 p, float c[3]) {
+// ------------------------------------------------------------------ textures ----
+// Rust `as isize` / `as u32` from f64: truncation toward zero, saturating, NaN -> 0
+__device__ __forceinline__ int64_t as_isize(double x) {
+    if (!(x == x)) return 0;
+    if (x >= 9223372036854775807.0) return INT64_MAX;
+    if (x <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)x;
+}
+__device__ __forceinline__ uint32_t as_u32(double x) {
+    if (!(x > 0.0)) return 0u;
+    if (x >= 4294967295.0) return 0xffffffffu;
+    return (uint32_t)x;
+}
+
+// Perlin::noise (noise.rs:111-148) + interpolate (:170-207). Sums start from 0.0 (f64 Sum).
+__device__ double perlin_noise(const DScene& S, const DPerlin& P, V3 p) {
+    const int64_t mask = (int64_t)P.point_count - 1;
+    const double* val = S.tex_f64 + P.voff;
+    const int32_t* px = S.tex_i32 + P.poff;
+    const int32_t* py = px + P.point_count;
+    const int32_t* pz = py + P.point_count;
+    if (P.smooth == RS_SMOOTH_NONE) {
+        const int64_t i = as_isize(4.0 * p.x) & mask, j = as_isize(4.0 * p.y) & mask, k = as_isize(4.0 * p.z) & mask;
+        const int idx = px[i] ^ py[j] ^ pz[k];
+        return P.vector ? val[3 * idx] : val[idx];
+    }
+    const int64_t i = as_isize(floor(p.x)), j = as_isize(floor(p.y)), k = as_isize(floor(p.z));
+    const double u = p.x - (double)i, v = p.y - (double)j, w = p.z - (double)k;
+    double uu = u, vv = v, ww = w;
+    if (P.smooth == RS_SMOOTH_HERMITE) {
+        uu = u * u * (3.0 - 2.0 * u);
+        vv = v * v * (3.0 - 2.0 * v);
+        ww = w * w * (3.0 - 2.0 * w);
+    }
+    double si = 0.0;
+    for (int di = 0; di < 2; ++di) {
+        double sj = 0.0;
+        for (int dj = 0; dj < 2; ++dj) {
+            double sk = 0.0;
+            for (int dk = 0; dk < 2; ++dk) {
+                const int64_t xi = (int64_t)((uint64_t)i + (uint64_t)di) & mask;  // wrapping add
+                const int64_t yi = (int64_t)((uint64_t)j + (uint64_t)dj) & mask;
+                const int64_t zi = (int64_t)((uint64_t)k + (uint64_t)dk) & mask;
+                const int idx = px[xi] ^ py[yi] ^ pz[zi];
+                double c;
+                if (P.vector) {
+                    const V3 weight = v3(u - (double)di, v - (double)dj, w - (double)dk);
+                    c = dot(ld3(val + 3 * idx), weight);
+                } else {
+                    c = val[idx];
+                }
+                sk = sk + fma((double)di, uu, (double)(1 - di) * (1.0 - uu)) *
+                              fma((double)dj, vv, (double)(1 - dj) * (1.0 - vv)) *
+                              fma((double)dk, ww, (double)(1 - dk) * (1.0 - ww)) * c;
+            }
+            sj = sj + sk;
+        }
+        si = si + sj;
+    }
+    return si;
+}
+// Perlin::calculate_turbulence (noise.rs:150-166)
+__device__ double perlin_turbulence(const DScene& S, const DPerlin& P, V3 p, int depth) {
+    double weight = 1.0, acc = 0.0;
+    for (int d = 0; d < depth; ++d) {
+        acc = acc + weight * perlin_noise(S, P, p);
+        weight *= 0.5;
+        p = v3(p.x * 2.0, p.y * 2.0, p.z * 2.0);
+    }
+    return fabs(acc);
+}
+// Perlin as a Texture (noise.rs:187-211): Color(1,1,1,1) * value (Color * f64 = channel * value as f32)
+__device__ __noinline__ double perlin_value(const DScene& S, const DPerlin& P, V3 point) {
+    if (P.type == RS_PERLIN_TURBULENCE) return perlin_turbulence(S, P, point, P.depth);
+    if (P.type == RS_PERLIN_MARBLE) {
+        const double noise = perlin_turbulence(S, P, point, P.depth);
+        return (rs_cr::sin_cr(fma(P.scale, point.z, 10.0 * noise)) + 1.0) * 0.5;
+    }
+    double noise = perlin_noise(S, P, v3(P.scale * point.x, P.scale * point.y, P.scale * point.z));
+    if (P.vector) noise = 0.5 * (noise + 1.0);
+    return noise;
+}
+
+// Image::color (image.rs:34-50) as packed 8-bit rgb (out of line, like perlin_value)
+__device__ __noinline__ uint32_t image_texel(const DScene& S, int id, double u, double v) {
+    const DImage I = S.images[id];
+    const double vv = 1.0 - v;
+    uint32_t x = as_u32(u * (double)I.w), y = as_u32(vv * (double)I.h);
+    if (x >= I.w) x = I.w - 1;
+    if (y >= I.h) y = I.h - 1;
+    const uint8_t* px = S.tex_u8 + I.off + 3 * ((uint64_t)y * I.w + x);
+    return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+}
+
+// texture eval: Color (color.rs:61-65) / Checker (checker.rs:21-30) / Perlin / Image (image.rs:34-50);
+// R = 0 (every scene mode but the rich one) compiles Color / Checker only
+template <int R>
+__device__ __forceinline__ void tex_color(const DScene& S, const DMaterial& m, V3 p, double u, double v, float c[3]) {
+    if (R && m.tex_kind == RS_TEX_PERLIN) {
+        const float f = (float)perlin_value(S, S.perlins[m.tex_data], p);
+        c[0] = 1.0f * f; c[1] = 1.0f * f; c[2] = 1.0f * f;
+        return;
+    }
+    if (R && m.tex_kind == RS_TEX_IMAGE) {
+        const uint32_t t = image_texel(S, m.tex_data, u, v);
+        c[0] = (float)(t & 255u) / 255.0f; c[1] = (float)((t >> 8) & 255u) / 255.0f; c[2] = (float)(t >> 16) / 255.0f;
+        return;
+    }
     bool odd = false;
     if (m.tex_kind == RS_TEX_CHECKER) {
         odd = rs_cr::sin3_negative(m.tex_scale * p.x, m.tex_scale * p.y, m.tex_scale * p.z);
@@ -491,6 +677,12 @@ __device__ __forceinline__ void tex_color(const DMaterial& m, V3 p, float c[3]) 
     const float* s = odd ? m.odd : m.even;
     c[0] = s[0]; c[1] = s[1]; c[2] = s[2];
 }
+template <int R>
+__device__ __forceinline__ void tex_color(const DScene& S, const DMaterial& m, const Hit& h, float c[3]) {
+    tex_color<R>(S, m, h.p, h.u, h.v, c);
+}
+
+// ------------------------------------------------------------------ materials ----
 
 // compiler-rt __powidf2 (phong powi with a runtime exponent)
 __device__ __forceinline__ double powi_rt(double a, int b) {

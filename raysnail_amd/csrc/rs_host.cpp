@@ -71,6 +71,16 @@ struct HObj {
     std::vector<rs_transform> tfs;     // XFORM
 };
 
+struct HPerlin {   // rs_perlin_desc with its tables copied
+    rs_perlin_desc d;
+    std::vector<double> values;
+    std::vector<int32_t> perms;        // perm_x, perm_y, perm_z
+};
+struct HImage {
+    uint32_t w = 0, h = 0;
+    std::vector<uint8_t> rgb;
+};
+
 typedef double M4[4][4];
 
 // vecmath 1.0.0 mat4_det / mat4_inv: explicit cofactor expansion, 1/det scaling.
@@ -141,6 +151,8 @@ void apply34(const M4 m, const double p[3], double w, double out[3]) {
 struct rs_scene {
     int device = 0;
     std::vector<rs_material_desc> mdesc;
+    std::vector<HPerlin> perlins;
+    std::vector<HImage> images;
     std::vector<HObj> objs;
     std::vector<uint32_t> world, lights;
     float bg_lo[3] = {0.3f, 0.4f, 0.5f}, bg_hi[3] = {0.7f, 0.89f, 1.0f};
@@ -254,6 +266,7 @@ struct rs_scene {
             return r;
         }
         case PK_SUB: return bbox_t((uint32_t)o.a, time0, time1);
+        case PK_MEDIUM: return bbox_t((uint32_t)o.a, time0, time1);  // constant.rs:93-95
         case PK_XFORM: {
             Box3 b = bbox_t((uint32_t)o.a, time0, time1);
             std::vector<std::vector<double>> fwd;
@@ -288,7 +301,7 @@ struct rs_scene {
         const HObj& o = objs[h];
         if (o.kind == PK_AND || o.kind == PK_SUB)
             return 1 + std::max(nest_depth((uint32_t)o.a), nest_depth((uint32_t)o.b));
-        if (o.kind == PK_XFORM) return 1 + nest_depth((uint32_t)o.a);
+        if (o.kind == PK_XFORM || o.kind == PK_MEDIUM) return 1 + nest_depth((uint32_t)o.a);
         return 0;
     }
 };
@@ -492,7 +505,8 @@ void commit(rs_scene* s) {
     for (const rs_material_desc& d : s->mdesc) {
         DMaterial m;
         std::memset(&m, 0, sizeof(m));
-        m.kind = d.kind; m.tex_kind = d.texture.kind; m.glass = d.glass;
+        m.kind = d.kind; m.tex_kind = d.texture.kind; m.tex_data = d.texture.data; m.glass = d.glass;
+        m.k_specular = d.k_specular;
         m.mix_a = d.mix_a; m.mix_b = d.mix_b;
         for (int i = 0; i < 4; ++i) { m.even[i] = d.texture.even[i]; m.odd[i] = d.texture.odd[i]; }
         m.tex_scale = d.texture.scale;
@@ -516,7 +530,9 @@ void commit(rs_scene* s) {
     // lights are needed when any pdf material can be hit (list.rs:51 would panic on % 0)
     bool needs_lights = false;
     for (const rs_material_desc& d : s->mdesc)
-        if (d.kind == RS_MAT_LAMBERTIAN || d.kind == RS_MAT_DIFFUSE_METAL || d.kind == RS_MAT_MIXED) needs_lights = true;
+        if (d.kind == RS_MAT_LAMBERTIAN || d.kind == RS_MAT_DIFFUSE_METAL || d.kind == RS_MAT_MIXED ||
+            d.kind == RS_MAT_ISOTROPIC || d.kind == RS_MAT_BLINN_PHONG)
+            needs_lights = true;
     for (uint32_t h : s->world) {
         const HObj& o = s->objs[h];
         if (o.mat == RS_NO_MATERIAL && o.kind <= PK_TRIANGLE) needs_lights = true;
@@ -529,6 +545,7 @@ void commit(rs_scene* s) {
     std::vector<DPrim> prims(s->objs.size());
     std::vector<DSphere> spheres; std::vector<DRect> rects; std::vector<DBox> boxes; std::vector<DQuadric> quads;
     std::vector<DTri> tris; std::vector<DCsg> csgs; std::vector<DXform> xforms; std::vector<DMat34> tf_f, tf_i;
+    std::vector<DMedium> media;
     for (size_t h = 0; h < s->objs.size(); ++h) {
         const HObj& o = s->objs[h];
         DPrim& P = prims[h];
@@ -578,6 +595,10 @@ void commit(rs_scene* s) {
             P.aux = (int32_t)o.tfs.size();
             P.idx = (int32_t)xforms.size(); xforms.push_back(x); break;
         }
+        case PK_MEDIUM: {
+            DMedium x; x.boundary = o.a; x.mat = o.mat; x.neg_inv_density = o.p[0];
+            P.idx = (int32_t)media.size(); media.push_back(x); break;
+        }
         default: throw Error(RS_E_INVALID, "unknown object kind");
         }
     }
@@ -607,7 +628,12 @@ void commit(rs_scene* s) {
     int nest = 0;
     for (uint32_t h : s->world) nest = std::max(nest, s->nest_depth(h));
     for (uint32_t h : s->lights) nest = std::max(nest, s->nest_depth(h));
-    s->scene_mode = s->spheres_only ? kSmSpheres : flat ? kSmFlat : nest == 0 ? kSmNest0 : nest <= 2 ? kSmNest2 : kSmGeneric;
+    // the rich features (ConstantMedium, Perlin / Image textures) exist only in the generic mode
+    bool rich = false;
+    for (const HObj& o : s->objs) rich = rich || o.kind == PK_MEDIUM;
+    for (const rs_material_desc& d : s->mdesc) rich = rich || d.texture.kind == RS_TEX_PERLIN || d.texture.kind == RS_TEX_IMAGE;
+    if (rich) s->spheres_only = false;
+    s->scene_mode = rich ? kSmGeneric : s->spheres_only ? kSmSpheres : flat ? kSmFlat : nest == 0 ? kSmNest0 : nest <= 2 ? kSmNest2 : kSmGeneric;
     bool all_monotone = true;
     for (uint32_t h : s->world) all_monotone = all_monotone && s->monotone(h);
     s->ref_order = !all_monotone;
@@ -696,6 +722,37 @@ void commit(rs_scene* s) {
     d.tf_fwd = upload(s, tf_f);
     d.tf_inv = upload(s, tf_i);
     d.mats = upload(s, mats);
+    d.media = upload(s, media);
+    d.has_media = media.empty() ? 0 : 1;
+    // texture tables: Perlin values / permutations, image pixels
+    std::vector<DPerlin> dper;
+    std::vector<double> tf64;
+    std::vector<int32_t> ti32;
+    for (const HPerlin& hp : s->perlins) {
+        DPerlin x;
+        std::memset(&x, 0, sizeof(x));
+        x.point_count = (int32_t)hp.d.point_count; x.vector = hp.d.vector; x.smooth = hp.d.smooth; x.type = hp.d.type;
+        x.depth = (int32_t)hp.d.depth; x.scale = hp.d.scale;
+        x.voff = (int32_t)tf64.size(); x.poff = (int32_t)ti32.size();
+        tf64.insert(tf64.end(), hp.values.begin(), hp.values.end());
+        ti32.insert(ti32.end(), hp.perms.begin(), hp.perms.end());
+        dper.push_back(x);
+    }
+    std::vector<DImage> dimg;
+    std::vector<uint8_t> tu8;
+    for (const HImage& hi : s->images) {
+        DImage x; x.w = hi.w; x.h = hi.h; x.off = tu8.size();
+        tu8.insert(tu8.end(), hi.rgb.begin(), hi.rgb.end());
+        dimg.push_back(x);
+    }
+    d.perlins = upload(s, dper);
+    d.tex_f64 = upload(s, tf64);
+    d.tex_i32 = upload(s, ti32);
+    d.images = upload(s, dimg);
+    d.tex_u8 = upload(s, tu8);
+    d.uv = 0;  // only the Image texture reads (u, v)
+    for (const DMaterial& m : mats) if (m.tex_kind == RS_TEX_IMAGE) d.uv = 1;
+    d.pad5 = 0;
     d.lights = upload(s, lights);
     d.n_lights = (int32_t)lights.size();
     d.root = root;
@@ -1021,6 +1078,11 @@ int rs_device_count(int* count) {
 uint64_t rs_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
     return splitmix64_h(splitmix64_h(splitmix64_h(splitmix64_h(seed) ^ (uint64_t)pass) ^ pixel) ^ (uint64_t)sample);
 }
+// Rng::medium_key + medium_uniform of rs_device.h
+double rs_medium_uniform(const uint32_t st[4], uint32_t handle) {
+    const uint64_t key = splitmix64_h((((uint64_t)st[1] << 32) | st[0]) ^ splitmix64_h(((uint64_t)st[3] << 32) | st[2]));
+    return (double)splitmix64_h(key ^ splitmix64_h(0x6d656469756d2121ULL + (uint64_t)handle)) * 0x1p-64;
+}
 
 int rs_scene_create(rs_scene** out) {
     return run([&] {
@@ -1045,14 +1107,73 @@ int rs_material(rs_scene* s, const rs_material_desc* d, int32_t* id) {
         S(s);
         if (!d || !id) throw Error(RS_E_INVALID, "null argument");
         if (s->committed) throw Error(RS_E_STATE, "scene already committed");
-        if (d->kind < RS_MAT_LAMBERTIAN || d->kind > RS_MAT_MIXED) throw Error(RS_E_INVALID, "unknown material kind");
-        if (d->texture.kind != RS_TEX_SOLID && d->texture.kind != RS_TEX_CHECKER) throw Error(RS_E_INVALID, "unknown texture kind");
+        if (d->kind < RS_MAT_LAMBERTIAN || d->kind > RS_MAT_BLINN_PHONG) throw Error(RS_E_INVALID, "unknown material kind");
+        if (d->texture.kind < RS_TEX_SOLID || d->texture.kind > RS_TEX_IMAGE) throw Error(RS_E_INVALID, "unknown texture kind");
+        if (d->texture.kind == RS_TEX_PERLIN && (d->texture.data < 0 || (size_t)d->texture.data >= s->perlins.size()))
+            throw Error(RS_E_INVALID, "texture refers to an unknown rs_perlin id");
+        if (d->texture.kind == RS_TEX_IMAGE && (d->texture.data < 0 || (size_t)d->texture.data >= s->images.size()))
+            throw Error(RS_E_INVALID, "texture refers to an unknown rs_image id");
         if (d->kind == RS_MAT_MIXED) {
             if (d->mix_a < 0 || (size_t)d->mix_a >= s->mdesc.size() || d->mix_b < 0 || (size_t)d->mix_b >= s->mdesc.size())
                 throw Error(RS_E_INVALID, "mixed material refers to unknown ids");
         }
         *id = (int32_t)s->mdesc.size();
         s->mdesc.push_back(*d);
+    });
+}
+int rs_perlin(rs_scene* s, const rs_perlin_desc* d, int32_t* id) {
+    return run([&] {
+        S(s);
+        if (!d || !id || !d->values || !d->perm_x || !d->perm_y || !d->perm_z) throw Error(RS_E_INVALID, "null argument");
+        if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+        const uint32_t n = d->point_count;
+        if (n == 0 || (n & (n - 1)) != 0 || n > (1u << 24)) throw Error(RS_E_INVALID, "point_count must be a power of two");
+        if (d->smooth < RS_SMOOTH_NONE || d->smooth > RS_SMOOTH_HERMITE || d->type < RS_PERLIN_NORMAL ||
+            d->type > RS_PERLIN_MARBLE || d->depth > 64)
+            throw Error(RS_E_INVALID, "bad Perlin smooth / type / depth");
+        HPerlin hp;
+        hp.d = *d;
+        hp.d.values = nullptr; hp.d.perm_x = hp.d.perm_y = hp.d.perm_z = nullptr;
+        hp.values.assign(d->values, d->values + (size_t)n * (d->vector ? 3 : 1));
+        for (const uint32_t* perm : {d->perm_x, d->perm_y, d->perm_z})
+            for (uint32_t i = 0; i < n; ++i) {
+                if (perm[i] >= n) throw Error(RS_E_INVALID, "Perlin permutation entry out of range");
+                hp.perms.push_back((int32_t)perm[i]);
+            }
+        *id = (int32_t)s->perlins.size();
+        s->perlins.push_back(std::move(hp));
+    });
+}
+int rs_image(rs_scene* s, const uint8_t* rgb, uint32_t width, uint32_t height, int32_t* id) {
+    return run([&] {
+        S(s);
+        if (!rgb || !id) throw Error(RS_E_INVALID, "null argument");
+        if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+        if (width == 0 || height == 0) throw Error(RS_E_INVALID, "empty image");
+        HImage hi;
+        hi.w = width; hi.h = height;
+        hi.rgb.assign(rgb, rgb + (size_t)width * height * 3);
+        *id = (int32_t)s->images.size();
+        s->images.push_back(std::move(hi));
+    });
+}
+int rs_constant_medium(rs_scene* s, uint32_t boundary, const float color[4], double density, uint32_t* out) {
+    return run([&] {
+        S(s)->check_handle(boundary);
+        if (!color || !out) throw Error(RS_E_INVALID, "null argument");
+        if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+        // ConstantMedium::new (constant.rs:29-39): material Isotropic(color), neg_inv_density = -1 / density
+        rs_material_desc m;
+        std::memset(&m, 0, sizeof(m));
+        m.kind = RS_MAT_ISOTROPIC;
+        m.texture.kind = RS_TEX_SOLID;
+        for (int i = 0; i < 4; ++i) m.texture.even[i] = m.texture.odd[i] = color[i];
+        m.texture.scale = 1.0; m.refractive = 1.0; m.multiplier = 1.0; m.mix_p = 0.5; m.phong_exponent = 1;
+        HObj o; o.kind = PK_MEDIUM; o.a = (int32_t)boundary;
+        o.mat = (int32_t)s->mdesc.size();
+        s->mdesc.push_back(m);
+        o.p[0] = -1.0 / density;
+        *out = s->add(o);
     });
 }
 int rs_sphere(rs_scene* s, const double c[3], double r, const double v[3], int32_t mat, uint32_t* out) {

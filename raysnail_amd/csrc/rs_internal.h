@@ -18,6 +18,9 @@ constexpr int kStackMax = 24;    // per-thread BVH stack entries (LDS, 24 KiB/bl
 // scratch); kSmGeneric -- up to RS_MAX_NEST levels.
 enum SceneMode { kSmGeneric = 0, kSmSpheres = 1, kSmFlat = 2, kSmNest0 = 3, kSmNest2 = 4 };
 constexpr int nest_of(int sm) { return sm == kSmNest0 ? 0 : sm == kSmNest2 ? 2 : sm == kSmGeneric ? RS_MAX_NEST : 0; }
+// the generic mode is also the rich one: ConstantMedium, Perlin / Image textures, (u, v) records
+// (commit puts every scene that uses them there; the other modes compile none of that code)
+constexpr int rich_of(int sm) { return sm == kSmGeneric ? 1 : 0; }
 
 struct PathParams {
     uint64_t n_items;

@@ -130,21 +130,23 @@ __device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere&
 // Nested-object entry points: Obj<L> instantiated only as deep as the scene mode needs.
 template <int SM>
 __device__ __forceinline__ bool obj_hit(const DScene& S, int p, const Ray& r, double tmin, double tmax, Hit& h) {
-    return Obj<nest_of(SM)>::hit(S, p, r, tmin, tmax, h);
+    return Obj<nest_of(SM), rich_of(SM)>::hit(S, p, r, tmin, tmax, h);
 }
 template <int SM>
 __device__ __forceinline__ V3 obj_random(const DScene& S, int p, V3 origin, Rng& rng) {
-    return Obj<nest_of(SM)>::random(S, p, origin, rng);
+    return Obj<nest_of(SM), rich_of(SM)>::random(S, p, origin, rng);
 }
 
 // Object hit for flat scenes (spheres, rects, triangles; no nesting): Obj<L>::hit's leaf cases only.
-__device__ __forceinline__ bool flat_hit(const DScene& S, const DPrim& P, const Ray& r, double tmin, double tmax, Hit& h) {
+// uv: compute the record's (u, v) (the winner's record when the scene reads them; never in traversal)
+__device__ __forceinline__ bool flat_hit(const DScene& S, const DPrim& P, const Ray& r, double tmin, double tmax, Hit& h,
+                                         int uv = 0) {
     if (P.kind == PK_TRIANGLE) return tri_hit(S.tris[P.idx], P.mat, r, tmin, tmax, h);
     if (P.kind == PK_RECT) {
         const DRect& R = S.rects[P.idx];
-        return rect_hit_raw(R.ax0, R.ax1, R.ax2, R.k, R.a0, R.a1, R.b0, R.b1, P.mat, r, tmin, tmax, h);
+        return rect_hit_raw(R.ax0, R.ax1, R.ax2, R.k, R.a0, R.a1, R.b0, R.b1, P.mat, r, tmin, tmax, h, uv);
     }
-    return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, tmax, h);
+    return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, tmax, h, uv);
 }
 
 // Leaf: the object is accepted iff its exact own bbox passes (aabb.rs:20-38, BVH leaf box) AND it
@@ -322,7 +324,7 @@ __device__ __forceinline__ bool finish_hit(const DScene& S, int bp, const Ray& r
     if (bp < 0) return false;
     if ((SM == kSmSpheres) || S.prims[bp].kind == PK_SPHERE) {
         const DPrim P = S.prims[bp];
-        return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, bend, h);
+        return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, bend, h, rich_of(SM) ? S.uv : 0);
     }
     if (SM == kSmFlat) return flat_hit(S, S.prims[bp], r, tmin, bend, h);
     return obj_hit<SM>(S, bp, r, tmin, bend, h);
@@ -353,7 +355,7 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
     float c[3];
     Pdf pdf;
     if (kind == RS_MAT_METAL) {  // metal.rs:104-118
-        tex_color(M, h.p, c);
+        tex_color<rich_of(SM)>(S, M, h, c);
         V3 rf = reflect_v(ray.d, h.n);
         if (!(dot(rf, h.n) > 0.0)) return false;
         T = v3(T.x * (double)c[0], T.y * (double)c[1], T.z * (double)c[2]);
@@ -386,16 +388,27 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
         ray.o = h.p; ray.d = nd;
         return true;
     } else if (kind == RS_MAT_LAMBERTIAN) {  // lambertian.rs:39-50
-        tex_color(M, h.p, c);
-        pdf.kind = 0;
+        tex_color<rich_of(SM)>(S, M, h, c);
+        pdf.kind = kPdfCosine;
         pdf.n = onb_from(h.n);
     } else if (kind == RS_MAT_DIFFUSE_METAL) {  // metal.rs:54-68
-        tex_color(M, h.p, c);
+        tex_color<rich_of(SM)>(S, M, h, c);
         V3 rf = reflect_v(ray.d, h.n);
         if (!(dot(rf, h.n) > 0.0)) return false;
-        pdf.kind = 1;
+        pdf.kind = kPdfReflection;
         pdf.exponent = M.exponent;
         pdf.refl = onb_from(rf);
+        pdf.n = onb_from(h.n);
+    } else if (kind == RS_MAT_ISOTROPIC) {  // isotropic.rs:25-33
+        c[0] = M.even[0]; c[1] = M.even[1]; c[2] = M.even[2];
+        pdf.kind = kPdfSphere;
+    } else if (kind == RS_MAT_BLINN_PHONG) {  // blinn_phong.rs:32-42 + BlinnPhongPdf::new (pdf.rs:153-172)
+        tex_color<rich_of(SM)>(S, M, h, c);
+        pdf.kind = kPdfBlinnPhong;
+        pdf.rin = ray.d;
+        pdf.exponent = M.exponent;
+        pdf.k = M.k_specular;
+        pdf.refl = onb_from(reflect_v(ray.d, h.n));
         pdf.n = onb_from(h.n);
     } else {
         return false;  // DiffuseLight reached through MixedMaterial: scatter None, no emission
@@ -408,8 +421,8 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
         pdf_val = 0.3183098861837907;
         const uint32_t li = rng.next_u32() % (uint32_t)S.n_lights;  // list.rs:49-52
         V3 rv;
-        if (SM == kSmSpheres) rv = Obj<0>::sphere_random(S.spheres[S.prims[S.lights[li]].idx], h.p, rng);
-        else if (SM == kSmFlat) rv = Obj<0>::random(S, S.lights[li], h.p, rng);  // no nesting below a leaf
+        if (SM == kSmSpheres) rv = Obj<0, 0>::sphere_random(S.spheres[S.prims[S.lights[li]].idx], h.p, rng);
+        else if (SM == kSmFlat) rv = Obj<0, 0>::random(S, S.lights[li], h.p, rng);  // no nesting below a leaf
         else rv = obj_random<SM>(S, S.lights[li], h.p, rng);
         V3 dl = unit(rv);
         if (M0.phong_factor > 0.0) light_multi += phong_highlight(-dl, ray.d, h.n, M0.phong_exponent, M0.phong_factor);
@@ -437,9 +450,10 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
 __device__ __forceinline__ V3 close_path(V3 L, V3 T) { return L + T * 0.0; }
 
 // DiffuseLight emission (light.rs:33-35) of the hit's material, as a radiance vector
-__device__ __forceinline__ V3 emission(const DMaterial& M0, V3 p) {
+template <int R>
+__device__ __forceinline__ V3 emission(const DScene& S, const DMaterial& M0, const Hit& h) {
     float c[3];
-    tex_color(M0, p, c);
+    tex_color<R>(S, M0, h, c);
     return v3((double)c[0] * M0.multiplier, (double)c[1] * M0.multiplier, (double)c[2] * M0.multiplier);
 }
 
@@ -456,7 +470,7 @@ __device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray,
     const int mi = h.mat >= 0 ? h.mat : S.default_mat;
     const DMaterial& M0 = S.mats[mi];
     if (M0.kind == RS_MAT_DIFFUSE_LIGHT) {  // scatter None -> emitted
-        V3 e = emission(M0, h.p);
+        V3 e = emission<rich_of(SM)>(S, M0, h);
         L = L + v3(T.x * e.x, T.y * e.y, T.z * e.z);
         return false;
     }
@@ -478,6 +492,7 @@ __device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, int
     for (uint32_t d = depth; d > 0; --d) {
         ++segs;
         Hit h;
+        if (rich_of(SM) && S.has_media) ray.key = rng.medium_key();
         const bool ok = world_hit<SM>(S, ray, 0.0001, h, stk);
         if (!shade_step<SM>(S, ok, h, ray, T, L, rng)) return L;
     }
@@ -650,7 +665,13 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DScene S, WfState W, uint3
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const Ray r = load_ray(cur, i);
+        Ray r = load_ray(cur, i);
+        if (rich_of(SM) && S.has_media) {  // the segment's medium key from the stored stream state
+            const uint4 g = cur.rng[i];
+            Rng rng;
+            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
+            r.key = rng.medium_key();
+        }
         double bend = RS_INF;
         const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
@@ -672,6 +693,9 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32
         uint32_t item = 0;
         if (i < n) {
             r = load_ray(cur, i);
+            const uint4 g = cur.rng[i];
+            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
+            if (rich_of(SM) && S.has_media) r.key = rng.medium_key();
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
@@ -679,8 +703,6 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32
             const D4 t4 = cur.thr[i], l4 = cur.rad[i];
             T = v3(t4.x, t4.y, t4.z);
             L = v3(l4.x, l4.y, l4.z);
-            const uint4 g = cur.rng[i];
-            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
             item = cur.item[i];
             alive = shade_step<SM>(S, ok, h, r, T, L, rng);
             if (alive && bounce + 1 >= depth) {  // depth limit
@@ -748,7 +770,7 @@ __global__ __launch_bounds__(kBlock, GEN ? 4 : RS_EXT_MIN_WAVES) void k_wfs_exte
                         const DPrim Pr = S.prims[bp];
                         Hit h;
                         sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
-                        add = emission(S.mats[Pr.mat >= 0 ? Pr.mat : S.default_mat], h.p);
+                        add = emission<0>(S, S.mats[Pr.mat >= 0 ? Pr.mat : S.default_mat], h);
                         cls = -1;
                     } else {
                         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
@@ -944,6 +966,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __
     if (i >= n) return;
     Ray r;
     r.o = ld3(rays + 7 * i); r.d = ld3(rays + 7 * i + 3); r.time = rays[7 * i + 6];
+    r.key = 0;  // probe rays: medium key 0 (orc_world_hit likewise)
     Hit h;
     double* o = out + 13 * (size_t)i;
     for (int k = 0; k < 13; ++k) o[k] = 0.0;
@@ -952,6 +975,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __
     if (world_hit<kSmGeneric>(S, r, tmin, h, stk_all + threadIdx.x) && h.t1 < tmax) {
         o[0] = 1.0; o[1] = h.t1; o[2] = h.t2;
         o[3] = h.p.x; o[4] = h.p.y; o[5] = h.p.z; o[6] = h.n.x; o[7] = h.n.y; o[8] = h.n.z;
+        o[9] = h.u; o[10] = h.v;
         o[11] = h.outside ? 1.0 : 0.0; o[12] = (double)h.mat;
     }
 }

@@ -19,6 +19,7 @@ enum PrimKind : int32_t {
     PK_AND = 5,     // csg Intersection  (src/hittable/csg/intersection.rs)
     PK_SUB = 6,     // csg Difference    (src/hittable/csg/difference.rs)
     PK_XFORM = 7,   // TfFacade          (src/hittable/transform/tf_facade.rs)
+    PK_MEDIUM = 8,  // ConstantMedium    (src/hittable/medium/constant.rs)
 };
 
 // One entry per hittable handle (world objects and nested children alike).
@@ -60,6 +61,12 @@ struct DCsg {      // Intersection(o1, o2) / Difference(plus, minus): prim indic
     int32_t a, b;
 };
 
+struct DMedium {   // ConstantMedium(boundary, Isotropic(color), density): constant.rs:13-39
+    int32_t boundary;        // prim index of the boundary object
+    int32_t mat;             // the Isotropic material created for it
+    double neg_inv_density;  // -1 / density
+};
+
 struct DXform {    // TfFacade: child prim + transforms [first, first+n) of the matrix table
     int32_t child;
     int32_t first;
@@ -73,6 +80,8 @@ struct DMat34 {
 struct DMaterial { // src/material/*.rs flattened
     int32_t kind;        // RS_MAT_*
     int32_t tex_kind;    // RS_TEX_*
+    int32_t tex_data;    // RS_TEX_PERLIN: DPerlin index; RS_TEX_IMAGE: DImage index
+    int32_t pad0;
     int32_t glass;
     int32_t mix_a, mix_b;
     int32_t phong_exponent;  // effective settings() (MixedMaterial -> material_1's)
@@ -84,6 +93,21 @@ struct DMaterial { // src/material/*.rs flattened
     double multiplier;
     double mix_p;
     double phong_factor;
+    double k_specular;   // BlinnPhong
+};
+
+struct DPerlin {   // noise.rs:28-37 (tables in DScene::tex_f64 / tex_i32)
+    int32_t point_count, vector, smooth, type;
+    int32_t depth;
+    int32_t voff;        // values: tex_f64[voff ..], 3 per point (vector) or 1
+    int32_t poff;        // perm_x, perm_y, perm_z: tex_i32[poff ..], point_count each
+    int32_t pad;
+    double scale;
+};
+
+struct DImage {    // image.rs: 8-bit RGB, row 0 = top, at DScene::tex_u8[off ..]
+    uint32_t w, h;
+    uint64_t off;
 };
 
 // Binary BVH node: both child boxes live in the parent, so one 64-byte fetch tests two children.
@@ -129,13 +153,21 @@ struct DScene {
     const DMat34* tf_fwd;
     const DMat34* tf_inv;
     const DMaterial* mats;
+    const DMedium* media;
+    const DPerlin* perlins;
+    const DImage* images;
+    const double* tex_f64;
+    const int32_t* tex_i32;
+    const uint8_t* tex_u8;
     const int32_t* lights;   // prim indices
     int32_t n_lights;
     int32_t root;            // root child code (node index, or ~prim if a single object, or INT32_MIN if empty)
     int32_t default_mat;     // world.rs:51 Lambertian(Color(1,1,1,1))
     int32_t ref_order;       // 1: traverse in BVH::hit's recursion order (bvh.rs:173-192); 0: near-first
     int32_t root4;           // root of nodes4 (>= 0) when the 4-wide tree is used, else -1
-    int32_t pad4;
+    int32_t uv;              // 1: hit records carry (u, v) (some texture reads them: Image)
+    int32_t has_media;       // 1: the scene has ConstantMedium objects (rays carry the medium key)
+    int32_t pad5;
     float bg_lo[4], bg_hi[4];
 };
 

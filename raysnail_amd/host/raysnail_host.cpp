@@ -14,10 +14,11 @@ namespace raysnail {
 namespace {
 thread_local std::string g_error;
 
-rs_texture_desc tex_desc(const Texture& t) {
+rs_texture_desc tex_desc(SceneSink& sink, const Texture& t) {
     rs_texture_desc d;
     std::memset(&d, 0, sizeof(d));
     d.kind = t.kind;
+    d.data = sink.texture_data(t);
     const float e[4] = {t.even.r, t.even.g, t.even.b, t.even.a};
     const float o[4] = {t.odd.r, t.odd.g, t.odd.b, t.odd.a};
     std::memcpy(d.even, e, sizeof(e));
@@ -44,6 +45,9 @@ const rsh_sink_api kHipApi = {
     [](void* s, uint32_t h) { return rs_lights_add(S(s), h); },
     [](void* s, const float* lo, const float* hi) { return rs_set_background(S(s), lo, hi); },
     [](void* s, double t0, double t1) { return rs_set_time_range(S(s), t0, t1); },
+    [](void* s, const rs_perlin_desc* d, int32_t* id) { return rs_perlin(S(s), d, id); },
+    [](void* s, const uint8_t* rgb, uint32_t w, uint32_t h, int32_t* id) { return rs_image(S(s), rgb, w, h, id); },
+    [](void* s, uint32_t b, const float* c, double d, uint32_t* h) { return rs_constant_medium(S(s), b, c, d, h); },
     []() { return rs_last_error(); },
 };
 
@@ -76,12 +80,36 @@ std::vector<uint32_t> SceneSink::object(const HittableRef& o) {
     return h;
 }
 
+int32_t SceneSink::texture_data(const Texture& t) {
+    const void* key = t.kind == RS_TEX_PERLIN ? (const void*)t.perlin.get() : t.kind == RS_TEX_IMAGE ? (const void*)t.image.get() : nullptr;
+    if (!key) {
+        if (t.kind == RS_TEX_PERLIN || t.kind == RS_TEX_IMAGE) throw Error(RS_E_INVALID, "texture without data");
+        return 0;
+    }
+    auto it = textures.find(key);
+    if (it != textures.end()) return it->second;
+    int32_t id = -1;
+    if (t.kind == RS_TEX_PERLIN) {
+        const PerlinData& p = *t.perlin;
+        rs_perlin_desc d;
+        std::memset(&d, 0, sizeof(d));
+        d.point_count = p.point_count; d.vector = p.vector ? 1 : 0; d.smooth = (int32_t)p.smooth; d.type = p.type;
+        d.depth = p.depth; d.scale = p.scale;
+        d.values = p.values.data(); d.perm_x = p.perm_x.data(); d.perm_y = p.perm_y.data(); d.perm_z = p.perm_z.data();
+        check(api.perlin(scene, &d, &id));
+    } else {
+        check(api.image(scene, t.image->rgb.data(), t.image->width, t.image->height, &id));
+    }
+    textures.emplace(key, id);
+    return id;
+}
+
 // ---------------------------------------------------------------------------------- materials ----
-rs_material_desc Material::base_desc(int32_t kind, const Texture& t) const {
+rs_material_desc Material::base_desc(SceneSink& sink, int32_t kind, const Texture& t) const {
     rs_material_desc d;
     std::memset(&d, 0, sizeof(d));
     d.kind = kind;
-    d.texture = tex_desc(t);
+    d.texture = tex_desc(sink, t);
     d.refractive = 1.0;
     d.exponent = 0.0;
     d.multiplier = 1.0;
@@ -97,27 +125,36 @@ static int32_t add_material(SceneSink& sink, const rs_material_desc& d) {
     return id;
 }
 
-int32_t Lambertian::export_to(SceneSink& sink) const { return add_material(sink, base_desc(RS_MAT_LAMBERTIAN, tex_)); }
-int32_t Metal::export_to(SceneSink& sink) const { return add_material(sink, base_desc(RS_MAT_METAL, tex_)); }
+int32_t Lambertian::export_to(SceneSink& sink) const { return add_material(sink, base_desc(sink, RS_MAT_LAMBERTIAN, tex_)); }
+int32_t Metal::export_to(SceneSink& sink) const { return add_material(sink, base_desc(sink, RS_MAT_METAL, tex_)); }
+int32_t Isotropic::export_to(SceneSink& sink) const {
+    return add_material(sink, base_desc(sink, RS_MAT_ISOTROPIC, Texture::color(color_)));
+}
+int32_t BlinnPhong::export_to(SceneSink& sink) const {
+    rs_material_desc d = base_desc(sink, RS_MAT_BLINN_PHONG, tex_);
+    d.k_specular = k_;
+    d.exponent = e_;
+    return add_material(sink, d);
+}
 int32_t DiffuseMetal::export_to(SceneSink& sink) const {
-    rs_material_desc d = base_desc(RS_MAT_DIFFUSE_METAL, tex_);
+    rs_material_desc d = base_desc(sink, RS_MAT_DIFFUSE_METAL, tex_);
     d.exponent = exponent_;
     return add_material(sink, d);
 }
 int32_t Dielectric::export_to(SceneSink& sink) const {
-    rs_material_desc d = base_desc(RS_MAT_DIELECTRIC, Texture::color(color_));
+    rs_material_desc d = base_desc(sink, RS_MAT_DIELECTRIC, Texture::color(color_));
     d.refractive = refractive_;
     d.glass = glass_ ? 1 : 0;
     return add_material(sink, d);
 }
 int32_t DiffuseLight::export_to(SceneSink& sink) const {
-    rs_material_desc d = base_desc(RS_MAT_DIFFUSE_LIGHT, tex_);
+    rs_material_desc d = base_desc(sink, RS_MAT_DIFFUSE_LIGHT, tex_);
     d.multiplier = mult_;
     return add_material(sink, d);
 }
 int32_t MixedMaterial::export_to(SceneSink& sink) const {
     const int32_t a = sink.material(m1_), b = sink.material(m2_);
-    rs_material_desc d = base_desc(RS_MAT_MIXED, Texture::color(Color{0.f, 0.f, 0.f, 1.f}));
+    rs_material_desc d = base_desc(sink, RS_MAT_MIXED, Texture::color(Color{0.f, 0.f, 0.f, 1.f}));
     d.mix_a = a;
     d.mix_b = b;
     d.mix_p = p_;
@@ -193,6 +230,23 @@ std::vector<uint32_t> Difference::export_to(SceneSink& sink) const {
     uint32_t h = 0;
     sink.check(sink.api.difference(sink.scene, a, b, sink.material(mat_), &h));
     return {h};
+}
+
+std::vector<uint32_t> ConstantMedium::export_to(SceneSink& sink) const {
+    const uint32_t b = single(sink.object(boundary_), "ConstantMedium");
+    const float c[4] = {color_.r, color_.g, color_.b, color_.a};
+    uint32_t h = 0;
+    sink.check(sink.api.constant_medium(sink.scene, b, c, density_, &h));
+    return {h};
+}
+
+BVH::BVH(const HittableList& list, std::pair<double, double>) : objects_(list.objects()) {}
+
+std::vector<uint32_t> BVH::export_to(SceneSink& sink) const {
+    std::vector<uint32_t> out;
+    for (const HittableRef& o : objects_)
+        for (uint32_t h : sink.object(o)) out.push_back(h);
+    return out;
 }
 
 std::vector<uint32_t> TfFacade::export_to(SceneSink& sink) const {

@@ -29,7 +29,8 @@ class rsh_sink_api(C.Structure):
     """struct rsh_sink_api (include/raysnail.hpp): the scene-building half of the C-ABI as a table."""
     _fields_ = [(name, C.c_void_p) for name in (
         "material", "sphere", "aarect", "box", "quadric", "triangles", "intersection", "difference",
-        "transformed", "world_add", "lights_add", "set_background", "set_time_range", "last_error")]
+        "transformed", "world_add", "lights_add", "set_background", "set_time_range", "perlin", "image",
+        "constant_medium", "last_error")]
 
 
 def sink_api_of(lib, prefix: str) -> rsh_sink_api:
@@ -65,6 +66,16 @@ def load() -> C.CDLL:
     lib.rsh_write_png.argtypes = [C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32]
     lib.rsh_write_png.restype = C.c_int
     lib.rsh_last_error.restype = C.c_char_p
+    lib.rsh_obj_load.argtypes = [C.c_char_p, C.c_double, C.POINTER(C.c_double), C.c_double, C.c_int,
+                                 C.POINTER(C.c_uint32), C.POINTER(C.POINTER(C.c_double)),
+                                 C.POINTER(C.POINTER(C.c_double))]
+    lib.rsh_obj_load.restype = C.c_int
+    lib.rsh_perlin_tables.argtypes = [C.c_uint64, C.c_uint32, C.c_int, C.c_void_p, C.c_void_p]
+    lib.rsh_perlin_tables.restype = C.c_int
+    lib.rsh_png_load.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                 C.POINTER(C.POINTER(C.c_uint8))]
+    lib.rsh_png_load.restype = C.c_int
+    lib.rsh_free.argtypes = [C.c_void_p]
     _LIB = lib
     return lib
 
@@ -108,3 +119,40 @@ def write_png(path: str, rgba: np.ndarray) -> None:
     rgba = np.ascontiguousarray(rgba, dtype=np.float32)
     h, w = rgba.shape[:2]
     _check(load().rsh_write_png(os.fsencode(path), rgba.ctypes.data_as(C.c_void_p), w, h))
+
+
+def obj_load(path: str, scale: float, offset, rotation_angle: float, axis: int):
+    """TriangleMesh::load's geometry: (n, 9) positions and (n, 9) vertex normals."""
+    lib = load()
+    n = C.c_uint32()
+    pos, nrm = C.POINTER(C.c_double)(), C.POINTER(C.c_double)()
+    _check(lib.rsh_obj_load(os.fsencode(path), float(scale), (C.c_double * 3)(*map(float, offset)),
+                            float(rotation_angle), int(axis), C.byref(n), C.byref(pos), C.byref(nrm)))
+    try:
+        P = np.ctypeslib.as_array(pos, shape=(n.value * 9,)).copy().reshape(-1, 9) if n.value else np.zeros((0, 9))
+        N = np.ctypeslib.as_array(nrm, shape=(n.value * 9,)).copy().reshape(-1, 9) if n.value else np.zeros((0, 9))
+    finally:
+        lib.rsh_free(pos)
+        lib.rsh_free(nrm)
+    return P, N
+
+
+def perlin_tables(seed: int, point_count: int, vector: bool):
+    """Perlin::new(point_count, vector, FastRng(seed)) tables: values and perm_x|perm_y|perm_z (uint32)."""
+    values = np.zeros(point_count * (3 if vector else 1), dtype=np.float64)
+    perms = np.zeros(3 * point_count, dtype=np.uint32)
+    _check(load().rsh_perlin_tables(int(seed), int(point_count), int(vector), values.ctypes.data_as(C.c_void_p),
+                                    perms.ctypes.data_as(C.c_void_p)))
+    return values, perms
+
+
+def png_load(path: str) -> np.ndarray:
+    """Image::new: decoded (H, W, 3) uint8."""
+    lib = load()
+    w, h = C.c_uint32(), C.c_uint32()
+    p = C.POINTER(C.c_uint8)()
+    _check(lib.rsh_png_load(os.fsencode(path), C.byref(w), C.byref(h), C.byref(p)))
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value * w.value * 3,)).copy().reshape(h.value, w.value, 3)
+    finally:
+        lib.rsh_free(p)

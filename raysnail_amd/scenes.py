@@ -8,7 +8,12 @@
   by any reference fixture ("raysnail-seed-7 (unverified restatement)").
 * sdl/example.sdl and sdl/quadric.sdl hand-translated with the CLI's conventions
   (src/bin/raysnail.rs:340-367: aperture 0.01, focus 10, light spheres r=12 x1.7, gradient background).
-* Cornell box (examples/common/scene.rs:211-334).
+* Cornell box (examples/common/scene.rs:211-334), with smoke (ConstantMedium boxes).
+* all_feature_scene (examples/common/scene.rs:336-469): boxes, moving sphere, glass / metal,
+  media, an Image-textured sphere (examples/earth-map.png when the reference tree is present, a
+  synthetic image of the same size otherwise) and a Perlin sphere.
+* materials_scene: a small build-owned scene exercising BlinnPhong, every Perlin variant, an Image
+  texture, an Isotropic medium and a Difference (GPU-vs-oracle parity fixture).
 """
 from __future__ import annotations
 
@@ -18,8 +23,11 @@ from typing import List, Tuple
 
 import numpy as np
 
-from .api import (AARect, AARectMetrics, Box, CameraBuilder, Checker, Color, Dielectric, DiffuseLight, DiffuseMetal,
-                  Glass, Gradient, HittableList, Intersection, Lambertian, Metal, Point3, Quadric, Sphere, TfFacade,
+import os
+
+from .api import (AARect, AARectMetrics, BVH, BlinnPhong, Box, CameraBuilder, Checker, Color, ConstantMedium,
+                  Dielectric, Difference, DiffuseLight, DiffuseMetal, Glass, Gradient, HittableList, Image,
+                  Intersection, Lambertian, Metal, Perlin, Point3, Quadric, SmoothType, Sphere, TfFacade,
                   Transform, TransformStack, TriangleMesh, World)
 
 M32 = 0xFFFFFFFF
@@ -385,4 +393,115 @@ def mesh_scene(width: int = 1920, height: int = 1080, n_theta: int = 120, n_phi:
     h.add(light)
     cam = CameraBuilder().look_from(Point3(0.0, 2.0, 5.0)).look_at(Point3(0.0, 0.9, 0.0)).fov(40.0) \
         .width(width).height(height).build()
+    return cam, World(h, lights, Gradient(C32(0.3, 0.4, 0.5), C32(0.7, 0.89, 1.0)), (0.0, 0.0))
+
+
+def cornell_smoke(width: int = 600, height: int = 600):
+    """cornell_box_scene(carton = true, carton_rotation = true, smoke = true) (scene.rs:211-334): the
+    light x7 over the larger rect, the two rotated boxes as ConstantMedium(white / black, 0.01)."""
+    red = Lambertian(C32(0.65, 0.05, 0.05))
+    green = Lambertian(C32(0.12, 0.45, 0.15))
+    white = Lambertian(C32(0.73, 0.73, 0.73))
+    light = DiffuseLight(C32(1.0, 1.0, 1.0)).multiplier(7.0)
+    o = HittableList()
+    o.add(AARect.new_yz(AARectMetrics(555.0, (0.0, 555.0), (0.0, 555.0)), green))
+    o.add(AARect.new_yz(AARectMetrics(0.0, (0.0, 555.0), (0.0, 555.0)), red))
+    o.add(AARect.new_xz(AARectMetrics(0.0, (0.0, 555.0), (0.0, 555.0)), white))
+    o.add(AARect.new_xz(AARectMetrics(555.0, (0.0, 555.0), (0.0, 555.0)), white))
+    o.add(AARect.new_xy(AARectMetrics(555.0, (0.0, 555.0), (0.0, 555.0)), white))
+    lrect = AARect.new_xz(AARectMetrics(554.0, (113.0, 443.0), (127.0, 432.0)), light)
+    o.add(lrect)
+    s1 = TransformStack(); s1.push(Transform.rotate_by_y_axis(-18.0)); s1.push(Transform.translate((130.0, 0.0, 65.0)))
+    s2 = TransformStack(); s2.push(Transform.rotate_by_y_axis(15.0)); s2.push(Transform.translate((265.0, 0.0, 295.0)))
+    box1 = TfFacade(Box((0.0, 0.0, 0.0), (165.0, 165.0, 165.0), white), s1)
+    box2 = TfFacade(Box((0.0, 0.0, 0.0), (165.0, 330.0, 165.0), white), s2)
+    o.add(ConstantMedium(box1, C32(1.0, 1.0, 1.0), 0.01))
+    o.add(ConstantMedium(box2, C32(0.0, 0.0, 0.0), 0.01))
+    cam = CameraBuilder().fov(40.0).look_from(Point3(278.0, 278.0, -800.0)).look_at(Point3(278.0, 278.0, 0.0)) \
+        .width(width).height(height).build()
+    lights = HittableList()
+    lights.add(lrect)
+    return cam, World(o, lights, Gradient(C32(0.0, 0.0, 0.0), C32(0.0, 0.0, 0.0)), (0.0, 0.0))
+
+
+def synthetic_image(width: int = 1920, height: int = 960, seed: int = 3) -> Image:
+    """A deterministic RGB image standing in for examples/earth-map.png where the reference tree is
+    absent (the GPU box): smooth bands plus noise, every byte value used."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:height, 0:width]
+    r = (127.5 + 127.5 * np.sin(x * 6.283185307179586 / width * 3.0)).astype(np.uint8)
+    g = (y * 255 // max(1, height - 1)).astype(np.uint8)
+    b = rng.integers(0, 256, (height, width), dtype=np.uint8)
+    return Image(np.stack([r, g, b], -1))
+
+
+EARTH_MAP = "/root/reference/examples/earth-map.png"
+
+
+def all_feature_scene(width: int = 800, height: int = 800, seed: int = 7, perlin_seed: int = 1, earth: Image = None):
+    """examples/common/scene.rs:336-469 (the book-2 final scene): 20x20 ground boxes in a BVH,
+    the xz light x7, a moving sphere, glass, metal, a glass sphere filled with ConstantMedium, a
+    global mist ConstantMedium, the earth-map sphere and a Perlin sphere. Upstream computes the
+    rotated 1000-sphere group but never adds it (scene.rs:452-458), so it is not here either.
+    Camera (478, 278, -600) -> (278, 278, 0), fov 40, shutter 1 (scene.rs:460-466); World time
+    range 0..1; lights = the xz rect; black background."""
+    rng = SeedRandom(seed)
+    ground = Lambertian(C32(0.48, 0.83, 0.53))
+    boxes1 = HittableList()
+    for i in range(20):
+        for j in range(20):
+            w = 100.0
+            x0, z0, y0 = -1000.0 + i * w, -1000.0 + j * w, 0.0
+            y1 = rng.range(1.0, 100.0)
+            boxes1.add(Box((x0, y0, z0), (x0 + w, y1, z0 + w), ground))
+    o = HittableList()
+    o.add(BVH(boxes1, (0.0, 1.0)))
+    light = AARect.new_xz(AARectMetrics(554.0, (123.0, 423.0), (147.0, 412.0)),
+                          DiffuseLight(C32(1.0, 1.0, 1.0)).multiplier(7.0))
+    o.add(light)
+    o.add(Sphere((400.0, 400.0, 200.0), 50.0, Lambertian(C32(0.7, 0.3, 0.1))).with_speed((30.0, 0.0, 0.0)))
+    o.add(Sphere((260.0, 150.0, 45.0), 50.0, Dielectric(C32(1.0, 1.0, 1.0), 1.5).reflect_curve(Glass())))
+    o.add(Sphere((0.0, 150.0, 145.0), 50.0, Metal(C32(0.8, 0.8, 0.9))))
+    o.add(Sphere((360.0, 170.0, 145.0), 70.0, Dielectric(C32(1.0, 1.0, 1.0), 1.5).reflect_curve(Glass())))
+    o.add(ConstantMedium(Sphere((360.0, 170.0, 145.0), 70.0, Lambertian(C32(1.0, 1.0, 1.0))),
+                         C32(0.2, 0.4, 0.9), 0.2))
+    o.add(ConstantMedium(Sphere((0.0, 0.0, 0.0), 5000.0, Dielectric(C32(1.0, 1.0, 1.0), 1.5).reflect_curve(Glass())),
+                         C32(1.0, 1.0, 1.0), 0.0001))
+    if earth is None:
+        earth = Image.new(EARTH_MAP) if os.path.exists(EARTH_MAP) else synthetic_image()
+    o.add(Sphere((400.0, 200.0, 400.0), 100.0, Lambertian(earth)))
+    tex = Perlin(256, True, perlin_seed).scale(0.1).smooth(SmoothType.HermitianCubic)
+    o.add(Sphere((220.0, 280.0, 300.0), 80.0, Lambertian(tex)))
+    cam = CameraBuilder().look_from(Point3(478.0, 278.0, -600.0)).look_at(Point3(278.0, 278.0, 0.0)).fov(40.0) \
+        .shutter_speed(1.0).width(width).height(height).build()
+    lights = HittableList()
+    lights.add(light)
+    return cam, World(o, lights, Gradient(C32(0.0, 0.0, 0.0), C32(0.0, 0.0, 0.0)), (0.0, 1.0))
+
+
+def materials_scene(width: int = 96, height: int = 64):
+    """Build-owned parity fixture: BlinnPhong (material settings with phong), Perlin in all three
+    types and smoothings (float and vector values), an Image texture on a sphere and on a rect,
+    an Isotropic medium inside a glass sphere, a Difference, a checker ground and a light sphere."""
+    h = HittableList()
+    h.add(Sphere((0.0, -1000.0, 0.0), 1000.0, Lambertian(Checker(C32(0.2, 0.3, 0.1), C32(0.9, 0.9, 0.9), 10.0))))
+    h.add(Sphere((-4.0, 1.0, 0.0), 1.0, BlinnPhong(0.5, 4.0, C32(0.99, 0.69, 0.2))))
+    h.add(Sphere((-2.0, 0.6, 2.0), 0.6, BlinnPhong(0.2, 40.0, Perlin(64, False, 5).smooth(SmoothType.None_).scale(3.0))))
+    h.add(Sphere((0.0, 1.0, 0.0), 1.0, Lambertian(Perlin(256, True, 2).scale(4.0).marble(5))))
+    h.add(Sphere((2.0, 0.7, 2.2), 0.7, Lambertian(Perlin(128, True, 9).turbulence(7))))
+    h.add(Sphere((0.5, 0.5, 2.8), 0.5, Lambertian(Perlin(32, False, 4).smooth(SmoothType.LinearInterpolate).scale(5.0))))
+    img = synthetic_image(64, 32, seed=11)
+    h.add(Sphere((4.0, 1.0, 0.0), 1.0, Lambertian(img)))
+    h.add(AARect.new_xy(AARectMetrics(-3.0, (-6.0, 6.0), (0.0, 4.0)), Lambertian(img)))
+    glass = Sphere((2.0, 1.2, -1.5), 1.2, Dielectric(C32(1.0, 1.0, 1.0), 1.5).reflect_curve(Glass()))
+    h.add(glass)
+    h.add(ConstantMedium(Sphere((2.0, 1.2, -1.5), 1.2, None), C32(0.2, 0.4, 0.9), 1.5))
+    h.add(Difference(Box((-1.5, 0.0, -2.5), (-0.5, 1.0, -1.5), Lambertian(C32(0.8, 0.2, 0.2))),
+                     Sphere((-1.0, 1.0, -2.0), 0.6, None), None))
+    lights = HittableList()
+    light = Sphere((10.0, 12.0, 8.0), 3.0, DiffuseLight(C32(1.0, 0.9, 0.7)).multiplier(4.0))
+    lights.add(light)
+    h.add(light)
+    cam = CameraBuilder().look_from(Point3(9.0, 3.0, 7.0)).look_at(Point3(0.0, 0.8, 0.0)).fov(35.0) \
+        .aperture(0.02).focus(10.0).width(width).height(height).build()
     return cam, World(h, lights, Gradient(C32(0.3, 0.4, 0.5), C32(0.7, 0.89, 1.0)), (0.0, 0.0))

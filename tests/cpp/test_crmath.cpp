@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <cmath>
 
 #include "../../include/rs_crmath.h"
 
@@ -46,6 +47,32 @@ int main(int argc, char** argv) {
         bad_sign += ref != rs_cr::sin3_negative(v[0], v[1], v[2]);
     }
     bad[5] += bad_sign;
+    // log of a uniform draw (ConstantMedium, medium/constant.rs:63); atan2 / asin of unit-vector
+    // components (Sphere::uv, sphere.rs:64-71) and of generic arguments
+    long bad_log = 0, bad_atan2 = 0, bad_asin = 0;
+    for (long i = 0; i < n; ++i) {
+        const double u = (double)g() * 0x1p-64;
+        if (u > 0.0 && rs_cr::log_cr(u) != (double)logq(u)) { ++bad_log; if (shown++ < 15) printf("log(%a) %a vs %a\n", u, rs_cr::log_cr(u), (double)logq(u)); }
+        const double x = u01(g) * 2.0 - 1.0, y = u01(g) * 2.0 - 1.0, z = u01(g) * 2.0 - 1.0;
+        const double l = std::sqrt(x * x + y * y + z * z);
+        if (l == 0.0 || l > 1.0) continue;
+        const double px = x / l, py = y / l, pz = z / l;
+        if (rs_cr::atan2_cr(-pz, px) != (double)atan2q(-pz, px)) { ++bad_atan2; if (shown++ < 20) printf("atan2(%a, %a) %a vs %a\n", -pz, px, rs_cr::atan2_cr(-pz, px), (double)atan2q(-pz, px)); }
+        if (rs_cr::asin_cr(py) != (double)asinq(py)) { ++bad_asin; if (shown++ < 25) printf("asin(%a) %a vs %a\n", py, rs_cr::asin_cr(py), (double)asinq(py)); }
+        const double ga = (u01(g) - 0.5) * std::ldexp(1.0, (int)(g() % 40) - 20), gb = (u01(g) - 0.5) * std::ldexp(1.0, (int)(g() % 40) - 20);
+        if (rs_cr::atan2_cr(ga, gb) != (double)atan2q(ga, gb)) ++bad_atan2;
+        const double ys = std::ldexp(u01(g), -(int)(g() % 30));
+        if (rs_cr::asin_cr(ys) != (double)asinq(ys)) ++bad_asin;
+    }
+    const double edge[] = {1.0, -1.0, 0x1.fffffffffffffp-1, 0.5, -0.5, 0x1p-30, 0x1p-1000};
+    for (double e : edge) bad_asin += rs_cr::asin_cr(e) != (double)asinq(e);
+    bad_log += rs_cr::log_cr(1.0) != 0.0;
+    bad_log += rs_cr::log_cr(0.0) != -INFINITY;
+    bad_atan2 += !(rs_cr::atan2_cr(0.0, -1.0) == (double)atan2q(0.0, -1.0) && rs_cr::atan2_cr(-0.0, 1.0) == 0.0 &&
+                   std::signbit(rs_cr::atan2_cr(-0.0, 1.0)));
+    bad_atan2 += rs_cr::atan2_cr(1.0, 0.0) != (double)atan2q(1.0, 0.0);
+    printf("n=%ld mismatches vs quad: log %ld atan2 %ld asin %ld\n", n, bad_log, bad_atan2, bad_asin);
+    bad[5] += bad_log + bad_atan2 + bad_asin;
     // special values
     long spec = 0;
     double s, c;
