@@ -97,7 +97,8 @@ __device__ __forceinline__ double medium_uniform(uint64_t key, int h) {
 struct Hit {
     V3 p, n;
     double t1, t2;
-    double u, v;   // computed only when the scene reads them (DScene::uv); 0 otherwise
+    double u, v;   // written only when the scene reads them (the `uv` flag of the hit functions: rich
+                   // scene mode with an Image texture); left unset otherwise, so they cost nothing
     int32_t mat;
     int32_t outside;
 };
@@ -109,7 +110,6 @@ __device__ __forceinline__ bool in_range(double t, double a, double b) { return 
 __device__ __forceinline__ void finish_rec(Hit& h, const Ray& r, double t1, double t2, V3 nrm, int32_t mat) {
     h.p = ray_at(r, t1);
     h.t1 = t1; h.t2 = t2; h.mat = mat;
-    h.u = 0.0; h.v = 0.0;
     bool outside = dot(r.d, nrm) < 0.0;
     h.n = outside ? nrm : -nrm;
     h.outside = outside;
@@ -211,7 +211,7 @@ __device__ V3 quadric_normal(const DQuadric& Q, V3 p) {
     return vdiv(rr, len);
 }
 // quadric.rs:112-182
-__device__ bool quadric_hit(const DQuadric& Q, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h) {
+__device__ bool quadric_hit(const DQuadric& Q, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h, int uv = 0) {
     const double* q = Q.q;
     const double qa = q[0], qb = q[1], qc = q[2], qd = q[3], qe = q[4], qf = q[5], qg = q[6], qh = q[7], qi = q[8], qj = q[9];
     double xo = r.o.x, yo = r.o.y, zo = r.o.z, xd = r.d.x, yd = r.d.y, zd = r.d.z;
@@ -237,6 +237,7 @@ __device__ bool quadric_hit(const DQuadric& Q, int32_t mat, const Ray& r, double
     }
     V3 p = ray_at(r, t1);
     finish_rec(h, r, t1, t2, quadric_normal(Q, p), mat);
+    if (uv) { h.u = 0.0; h.v = 0.0; }  // Quadric::uv (quadric.rs:106-110)
     return true;
 }
 __device__ __forceinline__ bool quadric_contains(const DQuadric& Q, V3 p) {  // quadric.rs:184-189
@@ -267,7 +268,7 @@ __device__ __forceinline__ bool tri_t(const DTri& T, const Ray& r, double tmin, 
     return true;
 }
 
-__device__ bool tri_hit(const DTri& T, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h) {
+__device__ bool tri_hit(const DTri& T, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h, int uv = 0) {
     double g = r.d.x, hh = r.d.y, i = r.d.z;
     double j = T.p0[0] - r.o.x, k = T.p0[1] - r.o.y, l = T.p0[2] - r.o.z;
     double eihf = T.e * i - hh * T.f;
@@ -286,7 +287,7 @@ __device__ bool tri_hit(const DTri& T, int32_t mat, const Ray& r, double tmin, d
     V3 n = ld3(T.n0) * (1.0 - beta - gamma) + ld3(T.n1) * beta + ld3(T.n2) * gamma;
     h.p = ray_at(r, t);
     h.n = n; h.t1 = t; h.t2 = RS_FMAX; h.mat = mat; h.outside = 1;   // with_normal
-    h.u = 0.0; h.v = 0.0;                                                // Triangle::uv (:80-82)
+    if (uv) { h.u = 0.0; h.v = 0.0; }                                    // Triangle::uv (:80-82)
     return true;
 }
 
@@ -327,8 +328,8 @@ template <int L, int R> struct Obj {
             return rect_hit_raw(Q.ax0, Q.ax1, Q.ax2, Q.k, Q.a0, Q.a1, Q.b0, Q.b1, P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         }
         case PK_BOX: return box_hit(S.boxes[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
-        case PK_QUADRIC: return quadric_hit(S.quadrics[P.idx], P.mat, r, tmin, tmax, h);
-        case PK_TRIANGLE: return tri_hit(S.tris[P.idx], P.mat, r, tmin, tmax, h);
+        case PK_QUADRIC: return quadric_hit(S.quadrics[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
+        case PK_TRIANGLE: return tri_hit(S.tris[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         case PK_AND: {  // csg/intersection.rs:58-100
             const DCsg C = S.csgs[P.idx];
             Hit h1, h2;
@@ -360,7 +361,7 @@ template <int L, int R> struct Obj {
                 V3 p = ray_at(r, hm.t2);
                 V3 n = shape_normal(S, C.b, p);
                 h.p = p; h.n = -n; h.mat = S.prims[C.b].mat; h.t1 = hm.t2; h.t2 = hp.t2; h.outside = 1;
-                h.u = 0.0; h.v = 0.0;
+                if (R) { h.u = 0.0; h.v = 0.0; }
             } else {
                 return false;
             }
@@ -373,7 +374,7 @@ template <int L, int R> struct Obj {
             rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
             rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
             rr.time = r.time;
-            rr.key = r.key;
+            if (R) rr.key = r.key;
             if (!Obj<L - 1, R>::hit(S, X.child, rr, tmin, tmax, h)) return false;
             h.p = tf_forward(S, X, P.aux, h.p, 1.0);
             return true;
@@ -539,10 +540,12 @@ __device__ __forceinline__ V3 phong_lobe(const Pdf& p, Rng& rng) {
     }
     return p.n.w;
 }
+// R = 0: only the cosine and reflection PDFs exist (Isotropic / BlinnPhong are rich-mode materials)
+template <int R>
 __device__ __forceinline__ double pdf_value(const Pdf& p, V3 d) {
     if (p.kind == kPdfCosine) { double c = dot(d, p.n.w); return c < 0.0 ? 0.0 : c / RS_PI; }
-    if (p.kind == kPdfSphere) return 1.0 / (4.0 * RS_PI);
-    if (p.kind == kPdfBlinnPhong) {  // pdf.rs:177-193
+    if (R && p.kind == kPdfSphere) return 1.0 / (4.0 * RS_PI);
+    if (R && p.kind == kPdfBlinnPhong) {  // pdf.rs:177-193
         const double cosine = dot(d, p.n.w);
         const V3 random_normal = unit(-p.rin + d);
         const double cosine_specular = fmax(dot(random_normal, p.n.w), 0.0);
@@ -552,10 +555,11 @@ __device__ __forceinline__ double pdf_value(const Pdf& p, V3 d) {
     double v = dot(d, p.refl.w) / RS_PI;
     return v < 0.0 ? 0.0 : v;
 }
+template <int R>
 __device__ __forceinline__ V3 pdf_generate(const Pdf& p, Rng& rng) {
     if (p.kind == kPdfCosine) return onb_local(p.n, random_cosine_direction(rng));
-    if (p.kind == kPdfSphere) return random_unit(rng);
-    if (p.kind == kPdfBlinnPhong) {  // pdf.rs:196-211
+    if (R && p.kind == kPdfSphere) return random_unit(rng);
+    if (R && p.kind == kPdfBlinnPhong) {  // pdf.rs:196-211
         if (rng.gen() < p.k) return phong_lobe(p, rng);
         return onb_local(p.n, random_cosine_direction(rng));
     }

@@ -628,10 +628,13 @@ void commit(rs_scene* s) {
     int nest = 0;
     for (uint32_t h : s->world) nest = std::max(nest, s->nest_depth(h));
     for (uint32_t h : s->lights) nest = std::max(nest, s->nest_depth(h));
-    // the rich features (ConstantMedium, Perlin / Image textures) exist only in the generic mode
+    // the rich features (ConstantMedium, Isotropic / BlinnPhong, Perlin / Image textures) exist only in
+    // the generic mode
     bool rich = false;
     for (const HObj& o : s->objs) rich = rich || o.kind == PK_MEDIUM;
-    for (const rs_material_desc& d : s->mdesc) rich = rich || d.texture.kind == RS_TEX_PERLIN || d.texture.kind == RS_TEX_IMAGE;
+    for (const rs_material_desc& d : s->mdesc)
+        rich = rich || d.texture.kind == RS_TEX_PERLIN || d.texture.kind == RS_TEX_IMAGE || d.kind == RS_MAT_ISOTROPIC ||
+               d.kind == RS_MAT_BLINN_PHONG;
     if (rich) s->spheres_only = false;
     s->scene_mode = rich ? kSmGeneric : s->spheres_only ? kSmSpheres : flat ? kSmFlat : nest == 0 ? kSmNest0 : nest <= 2 ? kSmNest2 : kSmGeneric;
     bool all_monotone = true;

@@ -25,6 +25,12 @@
 
 namespace rs {
 
+#ifdef RS_TRAV_STATS  // dev builds only (tools/build_variant.sh -DRS_TRAV_STATS): traversal counters
+__device__ unsigned long long g_trav_stats[8];
+#define RS_STAT(k, v) atomicAdd(&g_trav_stats[k], (unsigned long long)(v))
+__shared__ int s_st_nodes[256], s_st_leaves[256];
+#endif
+
 // aabb.rs:20-38 with inv = 1/d[i] precomputed per ray (the reference recomputes the same value
 // per node). Branch-free form: max/min over the three axes is equivalent to the early-exit loop
 // because t_min only grows and t_max only shrinks. This exact f64 test is applied to every
@@ -188,6 +194,18 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, 
 //    Each child box is tested when the recursion would visit it (the deferred right child is
 //    re-read from its parent when popped), so the tests see the same range as BVH::hit.
 // stk: this thread's column of the block's LDS stack (stride kBlock).
+#ifdef RS_TRAV_STATS
+// all 64 lanes converged: per ray sums, per wave the max node count (the wave runs the union of its
+// lanes' loops) and the wave's live lanes
+__device__ __forceinline__ void trav_stats_flush(bool live) {
+    int n = live ? s_st_nodes[threadIdx.x] : 0, l = live ? s_st_leaves[threadIdx.x] : 0, mx = n, cnt = live ? 1 : 0;
+    for (int off = 32; off > 0; off >>= 1) {
+        n += __shfl_xor(n, off, 64); l += __shfl_xor(l, off, 64); cnt += __shfl_xor(cnt, off, 64);
+        mx = max(mx, __shfl_xor(mx, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); }
+}
+#endif
 template <int SM>
 __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, int* stk) {
     if (S.root < 0) return -1;
@@ -198,8 +216,17 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
     int bp = -1;
     int node = S.root;
     int sp = 0;
+#ifdef RS_TRAV_STATS
+    int st_nodes = 0, st_leaves = 0;
+#define RS_ST_NODE() ++st_nodes
+#define RS_ST_LEAF() ++st_leaves
+#else
+#define RS_ST_NODE()
+#define RS_ST_LEAF()
+#endif
 #define RS_LEAF(code)                                                          \
     do {                                                                       \
+        RS_ST_LEAF();                                                          \
         const int bp_prev = bp;                                                \
         test_leaf<SM>(S, ~(code), r, tmin, best, bend, bp);                    \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
@@ -209,6 +236,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
         // children ordered by entry distance (nearest next, the rest pushed far-to-near).
         node = S.root4;
         while (true) {
+            RS_ST_NODE();
             const DNode4 N = S.nodes4[node];
             // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
             // and tested after the four box tests, when the node's registers are dead
@@ -246,11 +274,26 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
                 if (cnt > 3) { stk[sp * kBlock] = n2; ++sp; }
                 next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
             }
-            // leaves of this node (their hits only shrink the range the next node is tested with)
+            // leaves of this node (their hits only shrink the range the next node is tested with),
+            // in slot order through ONE copy of the leaf test: every lane tests its k-th leaf in
+            // the same pass, so a wave runs max-over-lanes leaf tests per node, not one pass per
+            // slot that any lane uses
+#ifdef RS_LEAF_PER_SLOT
             if (l0 != INT32_MIN) RS_LEAF(l0);
             if (l1 != INT32_MIN) RS_LEAF(l1);
             if (l2 != INT32_MIN) RS_LEAF(l2);
             if (l3 != INT32_MIN) RS_LEAF(l3);
+#else
+            while (true) {
+                int code;
+                if (l0 != INT32_MIN) { code = l0; l0 = INT32_MIN; }
+                else if (l1 != INT32_MIN) { code = l1; l1 = INT32_MIN; }
+                else if (l2 != INT32_MIN) { code = l2; l2 = INT32_MIN; }
+                else if (l3 != INT32_MIN) { code = l3; l3 = INT32_MIN; }
+                else break;
+                RS_LEAF(code);
+            }
+#endif
             if (next < 0) break;
             node = next;
         }
@@ -314,6 +357,10 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
         }
     }
 #undef RS_LEAF
+#ifdef RS_TRAV_STATS
+    s_st_nodes[threadIdx.x] = st_nodes;   // reduced per wave by the kernel (rs_trav_stats_flush)
+    s_st_leaves[threadIdx.x] = st_leaves;
+#endif
     bend_out = bend;
     return bp;
 }
@@ -399,10 +446,10 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
         pdf.exponent = M.exponent;
         pdf.refl = onb_from(rf);
         pdf.n = onb_from(h.n);
-    } else if (kind == RS_MAT_ISOTROPIC) {  // isotropic.rs:25-33
+    } else if (rich_of(SM) && kind == RS_MAT_ISOTROPIC) {  // isotropic.rs:25-33
         c[0] = M.even[0]; c[1] = M.even[1]; c[2] = M.even[2];
         pdf.kind = kPdfSphere;
-    } else if (kind == RS_MAT_BLINN_PHONG) {  // blinn_phong.rs:32-42 + BlinnPhongPdf::new (pdf.rs:153-172)
+    } else if (rich_of(SM) && kind == RS_MAT_BLINN_PHONG) {  // blinn_phong.rs:32-42 + BlinnPhongPdf::new (pdf.rs:153-172)
         tex_color<rich_of(SM)>(S, M, h, c);
         pdf.kind = kPdfBlinnPhong;
         pdf.rin = ray.d;
@@ -429,13 +476,14 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
         nr.o = ray_at(ray, h.t1 - 0.0002);
         nr.d = dl;
     } else {
-        V3 sd = (KIND == RS_MAT_LAMBERTIAN) ? onb_local(pdf.n, random_cosine_direction(rng)) : pdf_generate(pdf, rng);
-        pdf_val = pdf_value(pdf, sd);
+        V3 sd = (KIND == RS_MAT_LAMBERTIAN) ? onb_local(pdf.n, random_cosine_direction(rng))
+                                            : pdf_generate<rich_of(SM)>(pdf, rng);
+        pdf_val = pdf_value<rich_of(SM)>(pdf, sd);
         nr.o = h.p;
         nr.d = sd;
     }
     if (pdf_val <= 0.0 || pdf_val != pdf_val) pdf_val = 1e-5;
-    const double mult = pdf_value(pdf, nr.d) / pdf_val;
+    const double mult = pdf_value<rich_of(SM)>(pdf, nr.d) / pdf_val;
     T = v3(((double)c[0] * (light_multi * T.x)) * mult, ((double)c[1] * (light_multi * T.y)) * mult,
            ((double)c[2] * (light_multi * T.z)) * mult);
     ray = nr;
@@ -791,11 +839,42 @@ __global__ __launch_bounds__(kBlock, GEN ? 4 : RS_EXT_MIN_WAVES) void k_wfs_exte
                 }
             }
         }
+#ifdef RS_TRAV_STATS
+        trav_stats_flush(live);
+#endif
         if (GEN) block_slot1(live, &cnt[0]);  // segments at bounce 0 (stats)
         uint32_t* const cs[kClasses] = {&cnt[1], &cnt[2], &cnt[3], &cnt[4], &cnt[5]};
         const uint32_t slot = block_slot<kClasses>(cls, cs);
         if (cls >= 0) queues[cls][slot] = i;
     }
+}
+
+// Block-local reordering by a small key (0..2): lane p of the block is given the item of the p-th
+// lane in (key, wave, lane) order, so each wave holds items of one key except at key boundaries.
+// Pure scheduling: every item is still processed exactly once, by some lane of this block.
+__device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
+    __shared__ uint32_t wcnt[3][kBlock / 64];
+    __shared__ uint32_t perm[kBlock];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long mine = 0ull;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const unsigned long long m = __ballot(key == k);
+        if (key == k) mine = m;
+        if (lane == 0) wcnt[k][wave] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    uint32_t off = 0;
+    for (int k = 0; k < 3; ++k)
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t c = wcnt[k][w];
+            if (k < key || (k == key && w < wave)) off += c;
+        }
+    perm[off + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull))] = j;
+    __syncthreads();
+    const uint32_t r = perm[threadIdx.x];
+    __syncthreads();  // wcnt / perm are reused by the next call
+    return r;
 }
 
 template <int KIND>
@@ -808,7 +887,22 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
     const WfSet& cur = W.set[bounce & 1];
     const WfSet& nxt = W.set[(bounce + 1) & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        const uint32_t j = base + threadIdx.x;
+        uint32_t j = base + threadIdx.x;
+#ifdef RS_BRANCH_SORT  // measured: no gain on the bench frame (11.97 vs 11.80 ms)
+        if (KIND == RS_MAT_LAMBERTIAN || KIND == RS_MAT_DIFFUSE_METAL) {
+            // camera.rs:196-218 takes the light branch or the BSDF branch on the path's next draw
+            // (for these materials the first draw of the bounce); both are long, so peek that draw
+            // and group the block's paths by branch -- each wave then runs one branch
+            int key = 2;
+            if (j < n) {
+                const uint4 g = cur.rng[queue[j]];
+                Rng pk;
+                pk.x = g.x; pk.y = g.y; pk.z = g.z; pk.w = g.w;
+                key = pk.gen() < 0.5 ? 0 : 1;
+            }
+            j = block_sort3(key, j);
+        }
+#endif
         bool alive = false;
         Ray r;
         V3 T, L;
@@ -975,7 +1069,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __
     if (world_hit<kSmGeneric>(S, r, tmin, h, stk_all + threadIdx.x) && h.t1 < tmax) {
         o[0] = 1.0; o[1] = h.t1; o[2] = h.t2;
         o[3] = h.p.x; o[4] = h.p.y; o[5] = h.p.z; o[6] = h.n.x; o[7] = h.n.y; o[8] = h.n.z;
-        o[9] = h.u; o[10] = h.v;
+        if (S.uv) { o[9] = h.u; o[10] = h.v; }  // (u, v) exist only in scenes that read them
         o[11] = h.outside ? 1.0 : 0.0; o[12] = (double)h.mat;
     }
 }
@@ -1095,3 +1189,14 @@ hipError_t launch_finalize(const double* acc, float* out_rgba, const FinalParams
 }
 
 }  // namespace rs
+
+#ifdef RS_TRAV_STATS
+extern "C" int rs_debug_trav_stats(unsigned long long out[8], int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rs::g_trav_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -3;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rs::g_trav_stats), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    return 0;
+}
+#endif

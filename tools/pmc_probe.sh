@@ -1,14 +1,18 @@
 #!/bin/bash
-# counter passes on the bench frame (each pass its own rocprofv3 run, --pmc only)
+# counter passes on the bench frame (each pass its own rocprofv3 run, --pmc only); pass "list"
+# as $1 to also dump the available counter names
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/pmc_probe
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
+if [ "${1:-}" = "list" ]; then
+  timeout -s KILL 90 rocprofv3 -L > $OUT/counters.txt 2>&1 || echo "list failed (ignored)"
+fi
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_BRANCH" \
            "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE SQ_INSTS_VALU_FMA_F64" \
            "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum" ; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $set --output-format csv -d $OUT/p$i -o pmc -- python3 $R/tools/render_once.py 0 2 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $OUT/p$i -o pmc -- python3 $R/tools/render_once.py 0 2 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 echo done

@@ -1,0 +1,23 @@
+# dev: traversal counters of the bench frame from a -DRS_TRAV_STATS build (tools/build_variant.sh stats -DRS_TRAV_STATS)
+import ctypes as C, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from raysnail_amd import _abi
+lib_file = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "raysnail_amd/lib/var_stats.so")
+_abi.lib_path = lambda: lib_file
+import torch; torch.cuda.set_device(0)
+from raysnail_amd import scenes
+lib = _abi.load()
+out = (C.c_ulonglong * 8)()
+for name, build, spp, depth in (("rtow", lambda: scenes.rtow_13_1(800, 500)[:2], 64, 8),
+                                 ):
+    cam, world = build()
+    photo = cam.take_photo().samples(spp).depth(depth).seed(1)
+    photo.shot(None, world)
+    lib.rs_debug_trav_stats(out, 1)
+    photo.shot(None, world)
+    lib.rs_debug_trav_stats(out, 1)
+    nodes, leaves, rays, wmax, lanes, waves = out[:6]
+    print(f"{name}: rays {rays} nodes/ray {nodes/max(rays,1):.2f} leaves/ray {leaves/max(rays,1):.2f} "
+          f"wave-max nodes {wmax/max(waves,1):.2f} live lanes/wave {lanes/max(waves,1):.1f} "
+          f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f}", flush=True)
