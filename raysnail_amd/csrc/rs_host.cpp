@@ -684,14 +684,20 @@ void commit(rs_scene* s) {
         const Box3 b = s->bbox((uint32_t)h);
         for (int k = 0; k < 3; ++k) { pboxes[h].lo[k] = b.lo[k]; pboxes[h].hi[k] = b.hi[k]; }
     }
-    // wavefront shading class per prim (spheres-only scenes classify by the sphere's material)
+    // wavefront shading class per prim: the material of the record its hit produces (a TfFacade
+    // passes its child's record, tf_facade.rs:41-55); CSG records take either child's material or
+    // the CSG's own (set_material_if_none, hit.rs:69-78), so they go to the generic class 4
     std::vector<uint8_t> pclass(s->objs.size(), 4);
-    for (size_t h = 0; h < s->objs.size(); ++h) {
-        const int32_t m = s->objs[h].mat >= 0 ? s->objs[h].mat : default_mat;
+    std::function<int(uint32_t)> class_of = [&](uint32_t h) -> int {
+        const HObj& o = s->objs[h];
+        if (o.kind == PK_XFORM) return class_of((uint32_t)o.a);
+        if (o.kind == PK_AND || o.kind == PK_SUB || o.kind == PK_MEDIUM) return 4;
+        const int32_t m = o.mat >= 0 ? o.mat : default_mat;
         const int k = mats[m].kind;
-        pclass[h] = k == RS_MAT_LAMBERTIAN ? 0 : k == RS_MAT_METAL ? 1 : k == RS_MAT_DIFFUSE_METAL ? 2
-                  : k == RS_MAT_DIELECTRIC ? 3 : k == RS_MAT_DIFFUSE_LIGHT ? 6 : 4;
-    }
+        return k == RS_MAT_LAMBERTIAN ? 0 : k == RS_MAT_METAL ? 1 : k == RS_MAT_DIFFUSE_METAL ? 2
+             : k == RS_MAT_DIELECTRIC ? 3 : k == RS_MAT_DIFFUSE_LIGHT ? 6 : 4;
+    };
+    for (size_t h = 0; h < s->objs.size(); ++h) pclass[h] = (uint8_t)class_of((uint32_t)h);
     d.nodes = upload(s, dnodes);
     d.pbox = upload(s, pboxes);
     d.pclass = upload(s, pclass);
@@ -897,7 +903,11 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
     uint64_t n_chunks_total = 0;
     for (uint32_t s0 = 0; s0 < N; s0 += spb) n_chunks_total += ((uint64_t)n_pix * std::min(spb, N - s0) + chunk - 1) / chunk;
     WfState WS{};
-    const bool sorted = wavefront && s->spheres_only;   // material-sorted shading (spheres-only scenes)
+    // material-sorted shading (k_wfs_*) for the spheres / nest-0 / nest-2 modes; flat scenes (meshes)
+    // are traversal-bound and run faster on the plain wavefront, whose extend kernel is lighter
+    // (mesh 480x270x16: 5.8 vs 7.2 ms; example.sdl 8.8 -> 7.6 ms, quadric.sdl 9.9 -> 8.9 ms sorted)
+    const bool sorted = wavefront && (s->scene_mode == kSmSpheres || s->scene_mode == kSmNest0 ||
+                                      s->scene_mode == kSmNest2);
     const uint32_t cstride = sorted ? kWfsStride : 1;
     if (wavefront && N > 0) {
         WS = carve_wf(s, chunk);
@@ -950,15 +960,15 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
                     HIP_OK(hipEventRecord(kev[2 * ki], stream));
                     if (b == 0)
                         HIP_OK(launch_wfs_gen_extend(s->ds, dc, pp, WS, s->d_qptrs, cstride, c0, n, s->d_rad,
-                                                     std::min(wide, (n + kBlock - 1) / kBlock), stream));
+                                                     std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     else
                         HIP_OK(launch_wfs_extend(s->ds, WS, s->d_qptrs, b, cstride, pp.n_items, s->d_rad,
-                                                 std::min(wide, (n + kBlock - 1) / kBlock), stream));
+                                                 std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
                     ++ki;
                     for (int k = 0; k < kWfsClasses; ++k)
                         HIP_OK(launch_wfs_shade(s->ds, WS, s->qptr[k], k, b, cstride, st->depth, pp.n_items, s->d_rad,
-                                                std::min(wide, (n + kBlock - 1) / kBlock), stream));
+                                                std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     path_launches += 1 + kWfsClasses;
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
@@ -981,7 +991,7 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
     HIP_OK(launch_finalize(s->d_acc, d_out, fp, stream));
     unsigned long long cnt[512];
     HIP_OK(hipMemcpyAsync(cnt, s->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, stream));
-    const uint32_t cstride_f = (wavefront && s->spheres_only) ? kWfsStride : 1;
+    const uint32_t cstride_f = sorted ? kWfsStride : 1;
     std::vector<uint32_t> qc(wavefront && N > 0 ? (size_t)n_chunks_total * (st->depth + 1) * cstride_f : 0);
     if (!qc.empty()) HIP_OK(hipMemcpyAsync(qc.data(), s->d_counts, qc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));

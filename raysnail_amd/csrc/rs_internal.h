@@ -71,16 +71,17 @@ hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w
 hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st);
-// material-sorted variant (spheres-only scenes): counts stride per bounce = kWfsStride
+// material-sorted variant (every scene mode but the generic / rich one): counts stride per bounce = kWfsStride
 constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric, other
 constexpr uint32_t kWfsStride = 8;
 hipError_t launch_wfs_gen_extend(const DScene& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
-                                uint32_t blocks, hipStream_t st);
+                                uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
-                            uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);
+                            uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
-                           uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st);
+                           uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
+                           hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
 hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
 hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st);

@@ -11,6 +11,16 @@
 #include "rs_device.h"
 #include "rs_internal.h"
 
+// the material-sorted wavefront's scene modes (rs_host.cpp: spheres, nest-0, nest-2)
+#define RS_SM_SORTED_DISPATCH(sm, ...)                                     \
+    do {                                                                   \
+        switch (sm) {                                                      \
+        case kSmNest0: { constexpr int SMC = kSmNest0; __VA_ARGS__; break; }     \
+        case kSmNest2: { constexpr int SMC = kSmNest2; __VA_ARGS__; break; }     \
+        default: { constexpr int SMC = kSmSpheres; __VA_ARGS__; break; }         \
+        }                                                                  \
+    } while (0)
+
 // instantiate a launch for the scene mode (rs_internal.h SceneMode) as the constant SMC
 #define RS_SM_DISPATCH(sm, ...)                                            \
     do {                                                                   \
@@ -779,8 +789,8 @@ constexpr int kClsLight = 6;
 // GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
 // straight from registers, and only the paths that go on to shading are written (at index i, with
 // T = 1 and L = 0 implied for the bounce-0 shade kernels).
-template <bool GEN>
-__global__ __launch_bounds__(kBlock, GEN ? 4 : RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
+template <bool GEN, int SM>
+__global__ __launch_bounds__(kBlock, (GEN && SM == kSmSpheres) ? 4 : RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
@@ -807,7 +817,7 @@ __global__ __launch_bounds__(kBlock, GEN ? 4 : RS_EXT_MIN_WAVES) void k_wfs_exte
             }
             if (live) {
                 double bend = RS_INF;
-                const int bp = traverse<kSmSpheres>(S, r, 0.0001, bend, stk);
+                const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
                 V3 add;
                 bool done = true;
                 if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
@@ -815,10 +825,17 @@ __global__ __launch_bounds__(kBlock, GEN ? 4 : RS_EXT_MIN_WAVES) void k_wfs_exte
                 } else {
                     cls = (int)S.pclass[bp];
                     if (cls == kClsLight) {  // DiffuseLight: emitted, scatter None (camera.rs:172-176,250)
-                        const DPrim Pr = S.prims[bp];
                         Hit h;
-                        sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
-                        add = emission<0>(S, S.mats[Pr.mat >= 0 ? Pr.mat : S.default_mat], h);
+                        int mi;
+                        if (SM == kSmSpheres) {
+                            const DPrim Pr = S.prims[bp];
+                            sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
+                            mi = Pr.mat;
+                        } else {
+                            finish_hit<SM>(S, bp, r, 0.0001, bend, h);
+                            mi = h.mat;
+                        }
+                        add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
                         cls = -1;
                     } else {
                         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
@@ -877,7 +894,7 @@ __device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
     return r;
 }
 
-template <int KIND>
+template <int KIND, int SM>
 __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const uint32_t* __restrict__ queue,
                                                      int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
                                                      uint64_t n_items, double* __restrict__ rad) {
@@ -914,7 +931,7 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
-            finish_hit<kSmSpheres>(S, bp, r, 0.0001, hb.y, h);
+            finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
             if (bounce == 0) {  // fused gen+extend: T = 1, L = 0 not stored
                 T = v3(1.0, 1.0, 1.0);
                 L = v3(0.0, 0.0, 0.0);
@@ -930,14 +947,14 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
             const DMaterial& M0 = S.mats[mi];
             bool cont;
             if (KIND >= 0) {
-                cont = shade_surface<KIND, true>(S, h, M0, M0, r, T, rng);
+                cont = shade_surface<KIND, SM>(S, h, M0, M0, r, T, rng);
             } else {
                 int ms = mi;
                 for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {
                     const DMaterial& X = S.mats[ms];
                     ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
                 }
-                cont = shade_surface<-1, true>(S, h, M0, S.mats[ms], r, T, rng);
+                cont = shade_surface<-1, SM>(S, h, M0, S.mats[ms], r, T, rng);
             }
             alive = cont && (bounce + 1 < depth);
             if (!alive) {  // absorbed or depth limit: no emission term
@@ -1136,30 +1153,38 @@ hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, u
 }
 
 hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
-                            uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st) {
-    hipLaunchKernelGGL(k_wfs_extend<false>, dim3(blocks), dim3(kBlock), 0, st, s, w, queues, bounce, stride, n_items, rad,
-                       DCamera{}, PathParams{}, 0ull, 0u);
+                            uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<false, SMC>), dim3(blocks), dim3(kBlock), 0, st, s, w, queues,
+                                                 bounce, stride, n_items, rad, DCamera{}, PathParams{}, 0ull, 0u));
     return hipGetLastError();
 }
 
 hipError_t launch_wfs_gen_extend(const DScene& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
-                                uint32_t blocks, hipStream_t st) {
+                                uint32_t blocks, int sm, hipStream_t st) {
     if (!blocks) return hipSuccess;
-    hipLaunchKernelGGL(k_wfs_extend<true>, dim3(blocks), dim3(kBlock), 0, st, s, w, queues, 0u, stride, p.n_items, rad,
-                       c, p, item0, n);
+    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<true, SMC>), dim3(blocks), dim3(kBlock), 0, st, s, w, queues,
+                                                 0u, stride, p.n_items, rad, c, p, item0, n));
     return hipGetLastError();
 }
 
-hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
-                           uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st) {
+template <int SM>
+static void launch_wfs_shade_sm(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+                                uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks,
+                                hipStream_t st) {
     switch (cls) {
-    case 0: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_LAMBERTIAN>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 1: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_METAL>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 2: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_DIFFUSE_METAL>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 3: hipLaunchKernelGGL(k_wfs_shade<RS_MAT_DIELECTRIC>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    default: hipLaunchKernelGGL(k_wfs_shade<-1>, dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 0: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_LAMBERTIAN, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 1: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 2: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIFFUSE_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 3: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIELECTRIC, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    default: hipLaunchKernelGGL((k_wfs_shade<-1, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
     }
+}
+
+hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+                           uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
+                           hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, launch_wfs_shade_sm<SMC>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st));
     return hipGetLastError();
 }
 

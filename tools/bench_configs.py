@@ -25,6 +25,11 @@ def configs():
                lambda: scenes.quadric_sdl(1024, 1024), 1024, 50),
         "C5": ("synthetic 72k-triangle mesh + ground + light, 1920x1080, 512 -> 484 spp, depth 50",
                lambda: scenes.mesh_scene(1920, 1080), 512, 50),
+        # not BASELINE configs: the §8(f)3 features (rich scene mode) at a bench-like size
+        "X1": ("all_feature_scene (boxes, media, Image + Perlin spheres, moving sphere), 800x800, 64 spp, depth 50",
+               lambda: scenes.all_feature_scene(800, 800), 64, 50),
+        "X2": ("cornell_smoke (two ConstantMedium boxes), 600x600, 64 spp, depth 50",
+               lambda: scenes.cornell_smoke(600, 600), 64, 50),
     }
 
 

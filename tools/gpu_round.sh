@@ -8,10 +8,11 @@ TAG=${1:-r01}
 mkdir -p $OUT
 cd $R
 step() { local t=$1; shift; echo "== $* (limit ${t}s)" >> $OUT/steps.log; timeout -k 10 $t "$@"; local rc=$?; echo "   rc=$rc" >> $OUT/steps.log; return $rc; }
-step 600 python -m pytest tests -x -q -m gpu > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+step 600 python -u -m pytest tests -x -v --timeout 200 --timeout-method thread -m gpu > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 step 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o trace -- python3 $R/bench.py --steps 5 --warmup 2 --cpu-baseline 0 > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { echo "rocprof trace failed"; exit 1; }
 step 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-baseline 0 > /dev/null 2> $OUT/pmc_fetch.err || { echo "pmc fetch failed"; exit 1; }
 step 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-baseline 0 > /dev/null 2> $OUT/pmc_write.err || { echo "pmc write failed"; exit 1; }
+step 600 python $R/tools/bench_configs.py > $OUT/configs_$TAG.jsonl 2> $OUT/configs.err || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
 echo done
