@@ -826,7 +826,7 @@ void ensure(T*& p, size_t& cap, size_t n) {
 }
 
 WfState carve_wf(rs_scene* s, uint64_t cap) {
-    const size_t per_set = 4 * sizeof(D4) + sizeof(uint4) + sizeof(uint32_t);
+    const size_t per_set = 3 * sizeof(D4) + sizeof(uint32_t);
     const size_t per = 2 * per_set + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
     if (cap > s->wf_cap) {
         if (s->d_wf) HIP_OK(hipFree(s->d_wf));
@@ -842,8 +842,6 @@ WfState carve_wf(rs_scene* s, uint64_t cap) {
         t.ray_o = (D4*)p; p += sizeof(D4) * c;
         t.ray_d = (D4*)p; p += sizeof(D4) * c;
         t.thr = (D4*)p; p += sizeof(D4) * c;
-        t.rad = (D4*)p; p += sizeof(D4) * c;
-        t.rng = (uint4*)p; p += sizeof(uint4) * c;
         t.item = (uint32_t*)p; p += sizeof(uint32_t) * c;
         p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
     }
@@ -1034,19 +1032,19 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
         //  megakernel   : radiance out, 3 x f64 per sample
         //  wf extend    : ray in (2 x 32 B records) + hit out (16 B) per segment
         //  wfs extend   : bounces >= 1: ray in (64 B) per segment; + hit (16 B) + queue slot (4 B)
-        //                 per shaded segment; + throughput/radiance records in (64 B), item (4 B)
-        //                 and radiance out (24 B) per path ending in extend (sky miss / light hit).
+        //                 per shaded segment; + throughput record in (32 B), item (4 B) and
+        //                 radiance out (24 B) per path ending in extend (sky miss / light hit).
         //                 bounce 0 (fused with ray generation): radiance out (24 B) per sample that
-        //                 ends there (incl. masked); hit + queue slot + ray (64 B) + rng (16 B) +
-        //                 item (4 B) per shaded one
+        //                 ends there (incl. masked); hit + queue slot + ray records (64 B, rng
+        //                 inside) + throughput record (32 B) + item (4 B) per shaded one
         if (!wavefront) {
             stats->kernel_id = RS_KERNEL_PATH_MEGA;
             stats->kernel_bytes = 24ull * (uint64_t)n_pix * N;
         } else if (cstride_f > 1) {
             stats->kernel_id = RS_KERNEL_WFS_EXTEND;
             const uint64_t items = (uint64_t)n_pix * N, segr = seg - seg0, contr = cont - cont0;
-            stats->kernel_bytes = 24ull * (items - cont0) + 104ull * cont0 +
-                                  64ull * segr + 20ull * contr + 92ull * (segr - contr);
+            stats->kernel_bytes = 24ull * (items - cont0) + 120ull * cont0 +
+                                  64ull * segr + 20ull * contr + 60ull * (segr - contr);
         } else {
             stats->kernel_id = RS_KERNEL_WF_EXTEND;
             stats->kernel_bytes = 80ull * seg;

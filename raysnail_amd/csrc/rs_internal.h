@@ -39,13 +39,14 @@ struct alignas(32) D4 { double x, y, z, w; };
 
 // Wavefront path state (capacity = chunk size). 32-byte records per path per array, in two
 // ping-pong sets: bounce b reads set b&1 at [0, counts[b]) and the survivors are written,
-// compacted, into set (b+1)&1, so every kernel streams contiguous records.
+// compacted, into set (b+1)&1, so every kernel streams contiguous records. The XorShift128 state
+// rides in the fourth lanes of ray_d / thr (as bits). A live path's radiance is not stored: it is
+// always 0 (ray_color adds emission / background only where the recursion ends, camera.rs:172-254),
+// so a path's result is 0 + T * (its last term). 100 bytes per path and set.
 struct WfSet {
     D4* ray_o;            // origin xyz + time
-    D4* ray_d;            // direction xyz
-    D4* thr;              // throughput
-    D4* rad;              // radiance so far
-    uint4* rng;           // XorShift128 state
+    D4* ray_d;            // direction xyz + rng (x | y << 32)
+    D4* thr;              // throughput xyz + rng (z | w << 32)
     uint32_t* item;       // batch item (sample, pixel) of the path
 };
 struct WfState {

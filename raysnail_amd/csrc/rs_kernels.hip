@@ -103,6 +103,41 @@ __device__ __forceinline__ bool slab32(const float lo[3], const float hi[3], con
     return a <= b;
 }
 
+// 4-wide nodes: the ray's direction signs pick, per axis, which of the node's lo / hi planes is
+// the entry plane -- for inv >= 0 min(ax, bx) is ax (lo with o+d), else bx (hi with o-d), exactly
+// (fma is monotone in each operand) -- so a child costs 6 FMAs and four min / max instead of the
+// pairwise min / max of slab32. The plane arrays are fetched at per-ray byte offsets in DNode4.
+struct RayF4 {
+    float inv[3], nsub[3], fsub[3];   // entry / exit plane offsets ((o+d)*inv or (o-d)*inv)
+    uint32_t noff[3];                 // byte offset of the entry-plane array (lo_* or hi_*)
+};
+__device__ __forceinline__ RayF4 make_rayf4(const RayF& r) {
+    RayF4 q;
+    constexpr uint32_t lo_off[3] = {0, 16, 32}, hi_off[3] = {48, 64, 80};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool pos = r.inv[k] >= 0.0f;
+        q.inv[k] = r.inv[k];
+        q.nsub[k] = pos ? r.opi[k] : r.omi[k];
+        q.fsub[k] = pos ? r.omi[k] : r.opi[k];
+        q.noff[k] = pos ? lo_off[k] : hi_off[k];
+    }
+    return q;
+}
+// the exit-plane array is the other one of the axis: lo_off ^ hi_off = 48, 80, 112
+__device__ __forceinline__ uint32_t far_off(uint32_t noff, int k) { return noff ^ (k == 0 ? 48u : k == 1 ? 80u : 112u); }
+__device__ __forceinline__ bool slab4(float nx, float ny, float nz, float fx, float fy, float fz, const RayF4& r,
+                                      float tmin, float tmax, float& entry) {
+    const float ax = fmaf(nx, r.inv[0], -r.nsub[0]), bx = fmaf(fx, r.inv[0], -r.fsub[0]);
+    const float ay = fmaf(ny, r.inv[1], -r.nsub[1]), by = fmaf(fy, r.inv[1], -r.fsub[1]);
+    const float az = fmaf(nz, r.inv[2], -r.nsub[2]), bz = fmaf(fz, r.inv[2], -r.fsub[2]);
+    float a = fmaxf(fmaxf(fmaxf(tmin, ax), ay), az);
+    float b = fminf(fminf(fminf(tmax, bx), by), bz);
+    a = fmaf(-fabsf(a), 0x1p-18f, a);
+    b = fmaf(fabsf(b), 0x1p-18f, b);
+    entry = a;
+    return a <= b;
+}
 // Test one leaf object with the range [tmin, best); on acceptance best := its t1 (the
 // reference's right subtree is searched with `start..left.t1`, bvh.rs:179-188, i.e. the last
 // accepted hit sets the range end, which is the minimum except for Difference's back-face hits).
@@ -125,11 +160,24 @@ __device__ __forceinline__ bool sphere_t_trav(const DSphere& s, const Ray& r, do
     return false;
 }
 
+// Per-ray constants of the leaf tests, computed once per traversal: inv = 1 / d (the value
+// AABB::hit computes per node, aabb.rs:24) and a = |d|^2 (Sphere::hit's `a`, sphere.rs:88).
+struct RayC {
+    V3 inv;
+    double a;
+};
+__device__ __forceinline__ RayC ray_consts(const Ray& r) {
+    RayC c;
+    c.inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    c.a = len2(r.d);
+    return c;
+}
+
 // Sphere leaf: discriminant first, then the exact own box for spheres that hit.
-__device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int p, const Ray& r, double tmin,
-                                                 double& best, double& bend, int& bp) {
+__device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int p, const Ray& r, const RayC& rc,
+                                                 double tmin, double& best, double& bend, int& bp) {
     double t;
-    if (!sphere_t_trav(sp, r, len2(r.d), tmin, best, t)) return;
+    if (!sphere_t_trav(sp, r, rc.a, tmin, best, t)) return;
     double lo[3], hi[3];
     if (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0) {  // host: c -/+ r (sphere.rs:117-124)
         lo[0] = sp.c[0] - sp.r; lo[1] = sp.c[1] - sp.r; lo[2] = sp.c[2] - sp.r;
@@ -138,8 +186,7 @@ __device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere&
         const DBox64& B = S.pbox[p];
         lo[0] = B.lo[0]; lo[1] = B.lo[1]; lo[2] = B.lo[2]; hi[0] = B.hi[0]; hi[1] = B.hi[1]; hi[2] = B.hi[2];
     }
-    const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);  // the same value AABB::hit computes
-    if (!slab64(lo, hi, r.o, inv, tmin, best)) return;
+    if (!slab64(lo, hi, r.o, rc.inv, tmin, best)) return;
     bend = best; best = t; bp = p;
 }
 
@@ -169,26 +216,24 @@ __device__ __forceinline__ bool flat_hit(const DScene& S, const DPrim& P, const 
 // hits within [tmin, best). Both are pure, so the cheap test runs first: for spheres the
 // discriminant, and the exact box only for spheres that hit.
 template <int SM>
-__device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, double tmin, double& best, double& bend,
-                                          int& bp) {
+__device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, const RayC& rc, double tmin, double& best,
+                                          double& bend, int& bp) {
     if (SM == kSmSpheres) {  // prim-indexed sphere copy: one dependent load fewer than prims[p] -> spheres[idx]
-        test_sphere_leaf(S, S.psph[p], p, r, tmin, best, bend, bp);
+        test_sphere_leaf(S, S.psph[p], p, r, rc, tmin, best, bend, bp);
         return;
     }
     const DPrim P = S.prims[p];
     if (P.kind == PK_SPHERE) {
-        test_sphere_leaf(S, S.spheres[P.idx], p, r, tmin, best, bend, bp);
+        test_sphere_leaf(S, S.spheres[P.idx], p, r, rc, tmin, best, bend, bp);
     } else if (SM == kSmFlat && P.kind == PK_TRIANGLE) {  // triangle first (most leaves fail its beta test)
         double t;
         if (!tri_t(S.tris[P.idx], r, tmin, best, t)) return;
         const DBox64& B = S.pbox[p];
-        const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-        if (!slab64(B.lo, B.hi, r.o, inv, tmin, best)) return;
+        if (!slab64(B.lo, B.hi, r.o, rc.inv, tmin, best)) return;
         bend = best; best = t; bp = p;
     } else {
         const DBox64& B = S.pbox[p];
-        const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-        if (!slab64(B.lo, B.hi, r.o, inv, tmin, best)) return;
+        if (!slab64(B.lo, B.hi, r.o, rc.inv, tmin, best)) return;
         Hit tmp;
         const bool ok = SM == kSmFlat ? flat_hit(S, P, r, tmin, best, tmp) : obj_hit<SM>(S, p, r, tmin, best, tmp);
         if (ok) { bend = best; best = tmp.t1; bp = p; }
@@ -219,7 +264,8 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
 template <int SM>
 __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, int* stk) {
     if (S.root < 0) return -1;
-    const RayF rf = make_rayf(r.o, v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z));
+    const RayC rc = ray_consts(r);
+    const RayF rf = make_rayf(r.o, rc.inv);
     const float tmin32 = -round_up_f(-tmin);
     double best = RS_INF, bend = RS_INF;
     float best32 = __builtin_huge_valf();
@@ -238,36 +284,44 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
     do {                                                                       \
         RS_ST_LEAF();                                                          \
         const int bp_prev = bp;                                                \
-        test_leaf<SM>(S, ~(code), r, tmin, best, bend, bp);                    \
+        test_leaf<SM>(S, ~(code), r, rc, tmin, best, bend, bp);                \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
     if (S.root4 >= 0) {
         // 4-wide near-first: test the four child boxes of one 128-byte node, leaves at once, inner
         // children ordered by entry distance (nearest next, the rest pushed far-to-near).
         node = S.root4;
+        const RayF4 rq = make_rayf4(rf);
+        float4 NX, FX, NY, FY, NZ, FZ;
+        int4 NC;
+#define RS_FETCH4(nd)                                                                         \
+        {                                                                                     \
+            const char* nb = (const char*)(S.nodes4 + (nd));                                  \
+            NX = *(const float4*)(nb + rq.noff[0]); FX = *(const float4*)(nb + far_off(rq.noff[0], 0)); \
+            NY = *(const float4*)(nb + rq.noff[1]); FY = *(const float4*)(nb + far_off(rq.noff[1], 1)); \
+            NZ = *(const float4*)(nb + rq.noff[2]); FZ = *(const float4*)(nb + far_off(rq.noff[2], 2)); \
+            NC = *(const int4*)(nb + 96);                                                     \
+        }
         while (true) {
             RS_ST_NODE();
-            const DNode4 N = S.nodes4[node];
+            RS_FETCH4(node);
             // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
-            // and tested after the four box tests, when the node's registers are dead
-            int n0 = 0, n1 = 0, n2 = 0, n3 = 0;
-            int l0 = INT32_MIN, l1 = INT32_MIN, l2 = INT32_MIN, l3 = INT32_MIN;
-            float e0 = -__builtin_huge_valf(), e1 = e0, e2 = e0, e3 = e0;
-#define RS_SLOT_BODY(c, NK, EK, LK)                                                           \
-                if (c != INT32_MIN && slab32(lo, hi, rf, tmin32, best32, e)) {                \
-                    if (c < 0) { LK = c; } else { NK = c; EK = e; }                           \
-                }
+            // and tested after the four box tests, when the node's registers are dead. Branch-free:
+            // all four boxes are tested (the node's loads issue together) and the slot results are
+            // selects; an empty slot (INT32_MIN) is neither a leaf nor an inner child.
+            int n0, n1, n2, n3, l0, l1, l2, l3;
+            float e0, e1, e2, e3;
 #define RS_SLOT(K, NK, EK, LK)                                                                \
             {                                                                                 \
-                const float lo[3] = {N.lo_x[K], N.lo_y[K], N.lo_z[K]};                        \
-                const float hi[3] = {N.hi_x[K], N.hi_y[K], N.hi_z[K]};                        \
                 float e;                                                                      \
-                const int c = N.child[K];                                                     \
-                RS_SLOT_BODY(c, NK, EK, LK)                                                   \
+                const int c = NC.K;                                                           \
+                const bool hk = slab4(NX.K, NY.K, NZ.K, FX.K, FY.K, FZ.K, rq, tmin32, best32, e) & (c != INT32_MIN); \
+                LK = (hk & (c < 0)) ? c : INT32_MIN;                                          \
+                NK = c;                                                                       \
+                EK = (hk & (c >= 0)) ? e : -__builtin_huge_valf();                            \
             }
-            RS_SLOT(0, n0, e0, l0) RS_SLOT(1, n1, e1, l1) RS_SLOT(2, n2, e2, l2) RS_SLOT(3, n3, e3, l3)
+            RS_SLOT(x, n0, e0, l0) RS_SLOT(y, n1, e1, l1) RS_SLOT(z, n2, e2, l2) RS_SLOT(w, n3, e3, l3)
 #undef RS_SLOT
-#undef RS_SLOT_BODY
             const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
                             (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
             int next;
@@ -279,9 +333,12 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
 #define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
                 RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
 #undef RS_CS
-                if (cnt > 1) { stk[sp * kBlock] = n0; ++sp; }
-                if (cnt > 2) { stk[sp * kBlock] = n1; ++sp; }
-                if (cnt > 3) { stk[sp * kBlock] = n2; ++sp; }
+                // the cnt - 1 farther children are pushed; the writes above them are dead (the
+                // host keeps 3 * levels <= kStackMax, so sp + 2 stays inside the column)
+                stk[sp * kBlock] = n0;
+                stk[(sp + 1) * kBlock] = n1;
+                stk[(sp + 2) * kBlock] = n2;
+                sp += cnt - 1;
                 next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
             }
             // leaves of this node (their hits only shrink the range the next node is tested with),
@@ -307,6 +364,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
             if (next < 0) break;
             node = next;
         }
+#undef RS_FETCH4
     } else if ((SM == kSmSpheres) || !S.ref_order) {
         while (true) {
             const DNode N = S.nodes[node];
@@ -602,31 +660,45 @@ __global__ __launch_bounds__(kBlock) void k_path_mega(DScene S, DCamera C, PathP
 // load is 2 KiB contiguous). Bounce b: k_wf_extend traverses every path on queue b and writes
 // (prim, range end); k_wf_shade finishes the record, applies the material and appends the
 // surviving paths to queue b+1 with one atomic per wave (ballot + popcount prefix).
+// path records (rs_internal.h WfSet): two rng words as the bits of one double, never computed with
+__device__ __forceinline__ double pack_u32x2(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ void unpack_u32x2(double v, uint32_t& lo, uint32_t& hi) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    lo = (uint32_t)u;
+    hi = (uint32_t)(u >> 32);
+}
 __device__ __forceinline__ Ray load_ray(const WfSet& W, uint32_t p) {
     const D4 a = W.ray_o[p], b = W.ray_d[p];
     Ray r;
     r.o = v3(a.x, a.y, a.z); r.time = a.w;
     r.d = v3(b.x, b.y, b.z);
+    r.key = 0;
     return r;
 }
-__device__ __forceinline__ void store_path(const WfSet& W, uint32_t p, const Ray& r, const V3& T, const V3& L,
-                                           const Rng& rng, uint32_t item) {
-    D4 a, b, t, l;
-    a.x = r.o.x; a.y = r.o.y; a.z = r.o.z; a.w = r.time;
-    b.x = r.d.x; b.y = r.d.y; b.z = r.d.z; b.w = 0.0;
-    t.x = T.x; t.y = T.y; t.z = T.z; t.w = 0.0;
-    l.x = L.x; l.y = L.y; l.z = L.z; l.w = 0.0;
-    W.ray_o[p] = a; W.ray_d[p] = b; W.thr[p] = t; W.rad[p] = l;
-    W.rng[p] = make_uint4(rng.x, rng.y, rng.z, rng.w);
-    W.item[p] = item;
+__device__ __forceinline__ Rng load_rng(const WfSet& W, uint32_t p) {
+    Rng g;
+    unpack_u32x2(W.ray_d[p].w, g.x, g.y);
+    unpack_u32x2(W.thr[p].w, g.z, g.w);
+    return g;
 }
-// bounce-0 record of a fused gen+extend path: T = 1 and L = 0 are implied, not stored
-__device__ __forceinline__ void store_ray0(const WfSet& W, uint32_t p, const Ray& r, const Rng& rng, uint32_t item) {
-    D4 a, b;
+__device__ __forceinline__ void load_path(const WfSet& W, uint32_t p, Ray& r, V3& T, Rng& rng) {
+    const D4 a = W.ray_o[p], b = W.ray_d[p], t = W.thr[p];
+    r.o = v3(a.x, a.y, a.z); r.time = a.w;
+    r.d = v3(b.x, b.y, b.z);
+    r.key = 0;
+    T = v3(t.x, t.y, t.z);
+    unpack_u32x2(b.w, rng.x, rng.y);
+    unpack_u32x2(t.w, rng.z, rng.w);
+}
+__device__ __forceinline__ void store_path(const WfSet& W, uint32_t p, const Ray& r, const V3& T, const Rng& rng,
+                                           uint32_t item) {
+    D4 a, b, t;
     a.x = r.o.x; a.y = r.o.y; a.z = r.o.z; a.w = r.time;
-    b.x = r.d.x; b.y = r.d.y; b.z = r.d.z; b.w = 0.0;
-    W.ray_o[p] = a; W.ray_d[p] = b;
-    W.rng[p] = make_uint4(rng.x, rng.y, rng.z, rng.w);
+    b.x = r.d.x; b.y = r.d.y; b.z = r.d.z; b.w = pack_u32x2(rng.x, rng.y);
+    t.x = T.x; t.y = T.y; t.z = T.z; t.w = pack_u32x2(rng.z, rng.w);
+    W.ray_o[p] = a; W.ray_d[p] = b; W.thr[p] = t;
     W.item[p] = item;
 }
 
@@ -713,7 +785,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
         if (!live) { rad[item] = 0.0; rad[P.n_items + item] = 0.0; rad[2 * P.n_items + item] = 0.0; }
     }
     const uint32_t slot = block_slot1(live, &W.counts[0]);
-    if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), v3(0.0, 0.0, 0.0), rng, (uint32_t)item);
+    if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
 }
 
 template <int SM>
@@ -724,12 +796,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DScene S, WfState W, uint3
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         Ray r = load_ray(cur, i);
-        if (rich_of(SM) && S.has_media) {  // the segment's medium key from the stored stream state
-            const uint4 g = cur.rng[i];
-            Rng rng;
-            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
-            r.key = rng.medium_key();
-        }
+        if (rich_of(SM) && S.has_media) r.key = load_rng(cur, i).medium_key();  // the segment's medium key
         double bend = RS_INF;
         const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
@@ -746,21 +813,16 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32
         const uint32_t i = base + threadIdx.x;
         bool alive = false;
         Ray r;
-        V3 T, L;
+        V3 T, L = v3(0.0, 0.0, 0.0);  // a live path's radiance (WfSet)
         Rng rng;
         uint32_t item = 0;
         if (i < n) {
-            r = load_ray(cur, i);
-            const uint4 g = cur.rng[i];
-            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
+            load_path(cur, i, r, T, rng);
             if (rich_of(SM) && S.has_media) r.key = rng.medium_key();
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
             const bool ok = finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
-            const D4 t4 = cur.thr[i], l4 = cur.rad[i];
-            T = v3(t4.x, t4.y, t4.z);
-            L = v3(l4.x, l4.y, l4.z);
             item = cur.item[i];
             alive = shade_step<SM>(S, ok, h, r, T, L, rng);
             if (alive && bounce + 1 >= depth) {  // depth limit
@@ -770,7 +832,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32
             if (!alive) { rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z; }
         }
         const uint32_t slot = block_slot1(alive, &W.counts[bounce + 1]);
-        if (alive) store_path(nxt, slot, r, T, L, rng, item);
+        if (alive) store_path(nxt, slot, r, T, rng, item);
     }
 }
 
@@ -784,13 +846,12 @@ constexpr int kClsLight = 6;
 
 #ifndef RS_EXT_MIN_WAVES
 #define RS_EXT_MIN_WAVES 1  // 5 forces <=96 VGPRs but spills; measured slower (14.5 vs 13.8 ms)
-// (the fused bounce-0 variant asks for 4 waves: 128 VGPRs, no spill, instead of 132 at 3 waves)
 #endif
 // GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
 // straight from registers, and only the paths that go on to shading are written (at index i, with
 // T = 1 and L = 0 implied for the bounce-0 shade kernels).
 template <bool GEN, int SM>
-__global__ __launch_bounds__(kBlock, (GEN && SM == kSmSpheres) ? 4 : RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
+__global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
@@ -839,20 +900,20 @@ __global__ __launch_bounds__(kBlock, (GEN && SM == kSmSpheres) ? 4 : RS_EXT_MIN_
                         cls = -1;
                     } else {
                         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-                        if (GEN) store_ray0(cur, i, r, rng, item);
+                        if (GEN) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item);
                         done = false;
                     }
                 }
-                if (done) {
-                    D4 t4, l4;
+                if (done) {  // 0 + T * add: the path's radiance so far is 0 (WfSet)
+                    D4 t4;
                     if (GEN) {
-                        t4.x = t4.y = t4.z = 1.0; l4.x = l4.y = l4.z = 0.0;
+                        t4.x = t4.y = t4.z = 1.0;
                     } else {
-                        t4 = cur.thr[i]; l4 = cur.rad[i]; item = cur.item[i];
+                        t4 = cur.thr[i]; item = cur.item[i];
                     }
-                    rad[item] = l4.x + t4.x * add.x;
-                    rad[n_items + item] = l4.y + t4.y * add.y;
-                    rad[2 * n_items + item] = l4.z + t4.z * add.z;
+                    rad[item] = 0.0 + t4.x * add.x;
+                    rad[n_items + item] = 0.0 + t4.y * add.y;
+                    rad[2 * n_items + item] = 0.0 + t4.z * add.z;
                 }
             }
         }
@@ -912,9 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
             // and group the block's paths by branch -- each wave then runs one branch
             int key = 2;
             if (j < n) {
-                const uint4 g = cur.rng[queue[j]];
-                Rng pk;
-                pk.x = g.x; pk.y = g.y; pk.z = g.z; pk.w = g.w;
+                Rng pk = load_rng(cur, queue[j]);
                 key = pk.gen() < 0.5 ? 0 : 1;
             }
             j = block_sort3(key, j);
@@ -922,26 +981,16 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
 #endif
         bool alive = false;
         Ray r;
-        V3 T, L;
+        V3 T;
         Rng rng;
         uint32_t item = 0;
         if (j < n) {
             const uint32_t i = queue[j];
-            r = load_ray(cur, i);
+            load_path(cur, i, r, T, rng);
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
             finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
-            if (bounce == 0) {  // fused gen+extend: T = 1, L = 0 not stored
-                T = v3(1.0, 1.0, 1.0);
-                L = v3(0.0, 0.0, 0.0);
-            } else {
-                const D4 t4 = cur.thr[i], l4 = cur.rad[i];
-                T = v3(t4.x, t4.y, t4.z);
-                L = v3(l4.x, l4.y, l4.z);
-            }
-            const uint4 g = cur.rng[i];
-            rng.x = g.x; rng.y = g.y; rng.z = g.z; rng.w = g.w;
             item = cur.item[i];
             const int mi = h.mat >= 0 ? h.mat : S.default_mat;
             const DMaterial& M0 = S.mats[mi];
@@ -958,12 +1007,12 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
             }
             alive = cont && (bounce + 1 < depth);
             if (!alive) {  // absorbed or depth limit: no emission term
-                L = close_path(L, T);
+                const V3 L = close_path(v3(0.0, 0.0, 0.0), T);
                 rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
             }
         }
         const uint32_t slot = block_slot1(alive, &cnt_next[0]);
-        if (alive) store_path(nxt, slot, r, T, L, rng, item);
+        if (alive) store_path(nxt, slot, r, T, rng, item);
     }
 }
 
