@@ -788,8 +788,11 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
     if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
 }
 
+#ifndef RS_WF_EXT_FLAT_WAVES
+#define RS_WF_EXT_FLAT_WAVES 5  // flat scenes (meshes) are traversal-latency bound: keep 5 waves/SIMD
+#endif
 template <int SM>
-__global__ __launch_bounds__(kBlock) void k_wf_extend(DScene S, WfState W, uint32_t bounce) {
+__global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) void k_wf_extend(DScene S, WfState W, uint32_t bounce) {
     __shared__ int stk_all[kStackMax * kBlock];
     int* stk = stk_all + threadIdx.x;
     const uint32_t n = W.counts[bounce];
