@@ -175,6 +175,7 @@ struct rs_scene {
     int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
     uint32_t** d_qptrs = nullptr;                 // device array of the per-class queues
     uint32_t* qptr[kWfsClasses] = {nullptr};
+    uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
     uint64_t max_items_per_batch = 32ull << 20;  // RS_MAX_BATCH_ITEMS overrides (tests)
     int tree_depth = 0;
     double time0 = 0.0, time1 = 0.0;        // World::new time_limit (world.rs:40-53)
@@ -697,7 +698,11 @@ void commit(rs_scene* s) {
         return k == RS_MAT_LAMBERTIAN ? 0 : k == RS_MAT_METAL ? 1 : k == RS_MAT_DIFFUSE_METAL ? 2
              : k == RS_MAT_DIELECTRIC ? 3 : k == RS_MAT_DIFFUSE_LIGHT ? 6 : 4;
     };
-    for (size_t h = 0; h < s->objs.size(); ++h) pclass[h] = (uint8_t)class_of((uint32_t)h);
+    s->class_mask = 0;
+    for (size_t h = 0; h < s->objs.size(); ++h) {
+        pclass[h] = (uint8_t)class_of((uint32_t)h);
+        if (pclass[h] < kWfsClasses) s->class_mask |= 1u << pclass[h];
+    }
     d.nodes = upload(s, dnodes);
     d.pbox = upload(s, pboxes);
     d.pclass = upload(s, pclass);
@@ -853,6 +858,7 @@ WfState carve_wf(rs_scene* s, uint64_t cap) {
     HIP_OK(hipMemcpy(s->d_qptrs, qp, sizeof(qp), hipMemcpyHostToDevice));
     for (int k = 0; k < kWfsClasses; ++k) s->qptr[k] = qp[k];
     w.counts = nullptr;
+    w.cap = (uint32_t)c;
     return w;
 }
 
@@ -964,10 +970,13 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
                                                  std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
                     ++ki;
-                    for (int k = 0; k < kWfsClasses; ++k)
+                    ++path_launches;
+                    for (int k = 0; k < kWfsClasses; ++k) {
+                        if (!(s->class_mask & (1u << k))) continue;  // no prim of this class: empty queue
                         HIP_OK(launch_wfs_shade(s->ds, WS, s->qptr[k], k, b, cstride, st->depth, pp.n_items, s->d_rad,
                                                 std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
-                    path_launches += 1 + kWfsClasses;
+                        ++path_launches;
+                    }
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
                     HIP_OK(hipEventRecord(kev[2 * ki], stream));

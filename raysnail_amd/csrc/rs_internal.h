@@ -53,6 +53,7 @@ struct WfState {
     WfSet set[2];
     double2* hit;         // per compacted slot of the current bounce: (prim as bits, accepted range end)
     uint32_t* counts;     // [depth + 1] live paths per bounce
+    uint32_t cap;         // records per set (the sorted path fills a set from both ends, see k_wfs_shade)
 };
 
 struct FinalParams {
@@ -75,6 +76,9 @@ hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, u
 // material-sorted variant (every scene mode but the generic / rich one): counts stride per bounce = kWfsStride
 constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric, other
 constexpr uint32_t kWfsStride = 8;
+// counts[6] / counts[7] of a bounce: paths written from the front / the back of the set (light-
+// sample rays / the rest), so the next extend's waves hold rays of one kind (k_wfs_shade)
+constexpr int kCntFront = 6, kCntBack = 7;
 hipError_t launch_wfs_gen_extend(const DScene& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
                                 uint32_t blocks, int sm, hipStream_t st);

@@ -462,10 +462,11 @@ __device__ __forceinline__ double phong_highlight(V3 dir_to_light, V3 ray_dir, V
 // Scatter on a surface material (after MixedMaterial resolution) and the non-skip_pdf sampling
 // of camera.rs:176-247. KIND is the material class when known at compile time (material-sorted
 // wavefront shading) or -1 for a runtime switch. M0 = the hit's material (settings() source),
-// M = the material that scatters. Returns true when the path continues.
+// M = the material that scatters. Returns true when the path continues; *light_ray (when given)
+// is set to 1 if the next ray is a light sample.
 template <int KIND, int SM>
 __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, const DMaterial& M0, const DMaterial& M,
-                                              Ray& ray, V3& T, Rng& rng) {
+                                              Ray& ray, V3& T, Rng& rng, int* light_ray = nullptr) {
     const int kind = KIND >= 0 ? KIND : M.kind;
     float c[3];
     Pdf pdf;
@@ -533,6 +534,7 @@ __device__ __forceinline__ bool shade_surface(const DScene& S, const Hit& h, con
     Ray nr;
     nr.time = ray.time;
     if (rng.gen() < 0.5) {
+        if (light_ray) *light_ray = 1;
         pdf_val = 0.3183098861837907;
         const uint32_t li = rng.next_u32() % (uint32_t)S.n_lights;  // list.rs:49-52
         V3 rv;
@@ -861,13 +863,17 @@ __global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(DScene 
     __shared__ int stk_all[kStackMax * kBlock];
     int* stk = stk_all + threadIdx.x;
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
-    const uint32_t n = GEN ? n_gen : cnt[0];
+    const uint32_t nf = GEN ? 0u : cnt[kCntFront];
+    const uint32_t n = GEN ? n_gen : nf + cnt[kCntBack];
+    if (!GEN && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n;  // live paths at this bounce (stats)
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        const uint32_t i = base + threadIdx.x;
+        // thread -> record: the front run [0, nf), then the back run from the set's end down
+        const uint32_t j = base + threadIdx.x;
+        const uint32_t i = (GEN || j < nf) ? j : W.cap - 1u - (j - nf);
         int cls = -1;
         bool live = false;
-        if (i < n) {
+        if (j < n) {
             Ray r;
             Rng rng;
             uint32_t item = 0;
@@ -958,8 +964,11 @@ __device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
     return r;
 }
 
+#ifndef RS_LAMB_MIN_WAVES
+#define RS_LAMB_MIN_WAVES 4  // 130 -> 128 VGPRs (4 waves/SIMD, 12 B spill): 10.01 -> 9.94 ms bench frame
+#endif
 template <int KIND, int SM>
-__global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const uint32_t* __restrict__ queue,
+__global__ __launch_bounds__(kBlock, KIND == RS_MAT_LAMBERTIAN ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(DScene S, WfState W, const uint32_t* __restrict__ queue,
                                                      int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
                                                      uint64_t n_items, double* __restrict__ rad) {
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
@@ -983,6 +992,7 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
         }
 #endif
         bool alive = false;
+        int light_ray = 0;
         Ray r;
         V3 T;
         Rng rng;
@@ -999,14 +1009,14 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
             const DMaterial& M0 = S.mats[mi];
             bool cont;
             if (KIND >= 0) {
-                cont = shade_surface<KIND, SM>(S, h, M0, M0, r, T, rng);
+                cont = shade_surface<KIND, SM>(S, h, M0, M0, r, T, rng, &light_ray);
             } else {
                 int ms = mi;
                 for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {
                     const DMaterial& X = S.mats[ms];
                     ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
                 }
-                cont = shade_surface<-1, SM>(S, h, M0, S.mats[ms], r, T, rng);
+                cont = shade_surface<-1, SM>(S, h, M0, S.mats[ms], r, T, rng, &light_ray);
             }
             alive = cont && (bounce + 1 < depth);
             if (!alive) {  // absorbed or depth limit: no emission term
@@ -1014,8 +1024,11 @@ __global__ __launch_bounds__(kBlock) void k_wfs_shade(DScene S, WfState W, const
                 rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
             }
         }
-        const uint32_t slot = block_slot1(alive, &cnt_next[0]);
-        if (alive) store_path(nxt, slot, r, T, rng, item);
+        // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
+        // the front, the rest from the back: the next extend's waves then trace rays of one kind
+        uint32_t* const gc[2] = {&cnt_next[kCntBack], &cnt_next[kCntFront]};
+        const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
+        if (alive) store_path(nxt, light_ray ? slot : W.cap - 1u - slot, r, T, rng, item);
     }
 }
 
