@@ -968,7 +968,7 @@ __device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
 #define RS_LAMB_MIN_WAVES 4  // 130 -> 128 VGPRs (4 waves/SIMD, 12 B spill): 10.01 -> 9.94 ms bench frame
 #endif
 template <int KIND, int SM>
-__global__ __launch_bounds__(kBlock, KIND == RS_MAT_LAMBERTIAN ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(DScene S, WfState W, const uint32_t* __restrict__ queue,
+__global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest2) ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(DScene S, WfState W, const uint32_t* __restrict__ queue,
                                                      int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
                                                      uint64_t n_items, double* __restrict__ rad) {
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
