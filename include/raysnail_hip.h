@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 2
+#define RS_ABI_VERSION 3
 
 /* ---- status codes ---- */
 #define RS_OK             0
@@ -200,8 +200,24 @@ typedef struct rs_render_stats {
     double   kernel_ms;  /* device time of those launches (HIP events bracketing each launch) */
     uint64_t kernel_bytes;    /* algorithmic HBM bytes those launches move */
     int32_t  kernel_id;       /* RS_KERNEL_* */
-    int32_t  _pad;
+    int32_t  tree_arity;      /* BVH the traversal used: 4 = 4-wide, 2 = binary, 0 = empty world */
 } rs_render_stats;
+
+/* What rs_scene_commit built (diagnostic; no reference counterpart: BVH::new_internal,
+ * bvh.rs:58-113, builds its own binary tree). */
+typedef struct rs_scene_info {
+    int32_t  tree_arity;      /* 4: 4-wide tree, near-first traversal; 2: binary tree; 0: empty world */
+    int32_t  ref_order;       /* 1: the binary tree is walked in BVH::hit's recursion order (bvh.rs:173-192) */
+    int32_t  scene_mode;      /* kernel specialisation: 0 generic, 1 spheres, 2 flat, 3 nest-0, 4 nest-2 */
+    int32_t  tree_depth;      /* levels of the tree in use */
+    int32_t  stack_need;      /* exact worst-case traversal stack entries of that tree */
+    int32_t  stack_lds;       /* entries held in LDS; deeper ones spill to an HBM overflow array */
+    uint64_t n_nodes;         /* nodes of the tree in use */
+    uint64_t n_objects;       /* object handles (world objects, nested children, lights) */
+    uint64_t n_world;         /* objects in the world list (BVH leaves) */
+    int32_t  n_devices;       /* devices the scene is committed to */
+    int32_t  _pad;
+} rs_scene_info;
 
 typedef struct rs_scene rs_scene;
 
@@ -246,6 +262,16 @@ int rs_set_background(rs_scene* s, const float lo[3], const float hi[3]);
 int rs_set_time_range(rs_scene* s, double t0, double t1);
 /* freeze the scene: build the BVH and upload it to the current HIP device */
 int rs_scene_commit(rs_scene* s);
+/* freeze the scene for several devices (Painter::draw's thread fan-out, painter.rs:256-302 and the
+ * thread count of :318-325, moved to GPUs): the scene is built once and replicated to each listed
+ * HIP device ordinal. A device may be listed more than once (virtual devices with their own streams
+ * and buffers). Every rs_render / rs_render_device call then splits its row lattice over the
+ * devices the way render_rows interleaves rows over threads (device k of n takes lattice rows
+ * k, k+n, ..., painter.rs:248) and runs them concurrently; because every sample owns its RNG
+ * stream, the frame is bitwise independent of n. n = 0 is a host-only build: rs_scene_get_info
+ * works, rendering returns RS_E_STATE. */
+int rs_scene_commit_devices(rs_scene* s, const int* devices, int n);
+int rs_scene_get_info(const rs_scene* s, rs_scene_info* out);
 
 /* ---- render ---- */
 /* host output: out_rgba = W*H*4 floats; mask = W*H bytes or NULL (all pixels) */
@@ -253,7 +279,11 @@ int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* 
               const uint8_t* mask, float* out_rgba, rs_render_stats* stats);
 /* device output: d_out_rgba device pointer (W*H*4 floats), d_mask device pointer or NULL,
  * stream = hipStream_t or NULL (default stream). Returns after the work is enqueued AND
- * complete (the call synchronises its stream) so that stats are final. */
+ * complete (the call synchronises its stream) so that stats are final. With several devices
+ * (rs_scene_commit_devices) d_out_rgba, d_mask and stream belong to the FIRST listed device, which
+ * renders its rows in place; the other devices render on their own streams and copy their rows
+ * into d_out_rgba at frame end (peer access where the devices allow it). Stats are summed over
+ * the devices (kernel_ms / path_ms are device time, ms is the call's wall time). */
 int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st,
                      const uint8_t* d_mask, float* d_out_rgba, void* stream, rs_render_stats* stats);
 

@@ -95,7 +95,14 @@ class rs_noise_stats(C.Structure):
 class rs_render_stats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("ms", C.c_double), ("path_ms", C.c_double),
                 ("launches", C.c_uint32), ("kernel_launches", C.c_uint32), ("kernel_ms", C.c_double),
-                ("kernel_bytes", C.c_uint64), ("kernel_id", C.c_int32), ("_pad", C.c_int32)]
+                ("kernel_bytes", C.c_uint64), ("kernel_id", C.c_int32), ("tree_arity", C.c_int32)]
+
+
+class rs_scene_info(C.Structure):
+    _fields_ = [("tree_arity", C.c_int32), ("ref_order", C.c_int32), ("scene_mode", C.c_int32),
+                ("tree_depth", C.c_int32), ("stack_need", C.c_int32), ("stack_lds", C.c_int32),
+                ("n_nodes", C.c_uint64), ("n_objects", C.c_uint64), ("n_world", C.c_uint64),
+                ("n_devices", C.c_int32), ("_pad", C.c_int32)]
 
 
 KERNEL_NAMES = {0: None, 1: "k_path_mega", 2: "k_wf_extend", 3: "k_wfs_extend"}
@@ -172,10 +179,12 @@ def load() -> C.CDLL:
     lib.rs_render_device.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), VP, VP, VP,
                                      C.POINTER(rs_render_stats)]
     lib.rs_probe_world_hit.argtypes = [VP, VP, C.c_uint32, C.c_double, C.c_double, VP]
-    for fn in ("rs_probe_world_hit", "rs_scene_create", "rs_scene_destroy", "rs_scene_commit", "rs_render", "rs_render_device",
+    lib.rs_scene_get_info.argtypes = [VP, C.POINTER(rs_scene_info)]
+    lib.rs_scene_commit_devices.argtypes = [VP, C.POINTER(C.c_int), C.c_int]
+    for fn in ("rs_probe_world_hit", "rs_scene_get_info", "rs_scene_commit_devices", "rs_scene_create", "rs_scene_destroy", "rs_scene_commit", "rs_render", "rs_render_device",
                "rs_device_count"):
         getattr(lib, fn).restype = C.c_int
-    if lib.rs_abi_version() != 2:
+    if lib.rs_abi_version() != 3:
         raise RuntimeError("libraysnail_hip.so ABI mismatch")
     _LIB = lib
     return lib
@@ -186,6 +195,6 @@ EXPORTED_SYMBOLS = [
     "rs_abi_version", "rs_last_error", "rs_device_count", "rs_stream_key", "rs_medium_uniform", "rs_scene_create",
     "rs_scene_destroy", "rs_perlin", "rs_image", "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
     "rs_difference", "rs_transformed", "rs_constant_medium", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
-    "rs_scene_commit", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
+    "rs_scene_commit", "rs_scene_commit_devices", "rs_scene_get_info", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
     "rs_probe_world_hit", "rs_probe_samples",
 ]

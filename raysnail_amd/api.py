@@ -520,13 +520,19 @@ def realize(world: World, lib, handle, prefix: str = "rs_") -> None:
 class DeviceScene:
     """A committed libraysnail_hip scene (BVH + SoA scene data resident in HBM)."""
 
-    def __init__(self, world: World):
+    def __init__(self, world: World, devices: Optional[Sequence[int]] = None):
+        """devices: None = the current HIP device (rs_scene_commit); a list of HIP ordinals (repeats
+        allowed: virtual devices) = rs_scene_commit_devices; [] = host-only build (info() only)."""
         self.lib = A.load()
         h = C.c_void_p()
         _check(self.lib, self.lib.rs_scene_create(C.byref(h)), "rs_")
         self.handle = h
         realize(world, self.lib, h, "rs_")
-        _check(self.lib, self.lib.rs_scene_commit(h), "rs_")
+        if devices is None:
+            _check(self.lib, self.lib.rs_scene_commit(h), "rs_")
+        else:
+            devs = (C.c_int * max(1, len(devices)))(*devices)
+            _check(self.lib, self.lib.rs_scene_commit_devices(h, devs, len(devices)), "rs_")
 
     def __del__(self):
         try:
@@ -535,6 +541,12 @@ class DeviceScene:
                 self.handle = None
         except Exception:
             pass
+
+    def info(self) -> A.rs_scene_info:
+        """What commit built: tree arity / depth, exact stack need, scene mode (rs_scene_get_info)."""
+        inf = A.rs_scene_info()
+        _check(self.lib, self.lib.rs_scene_get_info(self.handle, C.byref(inf)), "rs_")
+        return inf
 
     def render(self, cam: A.rs_camera_desc, st: A.rs_render_settings, mask: Optional[np.ndarray] = None,
                out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, A.rs_render_stats]:

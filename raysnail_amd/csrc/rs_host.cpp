@@ -148,8 +148,51 @@ void apply34(const M4 m, const double p[3], double w, double out[3]) {
 
 }  // namespace
 
-struct rs_scene {
+// The committed scene in device layout, built once on the host: the DScene template (scalars set,
+// pointers null) plus one byte blob per device array and the DScene field that points to it.
+struct Blob {
+    size_t field_off;            // offset of the pointer field in DScene
+    std::vector<char> bytes;
+};
+struct HostScene {
+    DScene ds{};
+    std::vector<Blob> blobs;
+};
+
+// One device the scene is committed to: its copy of the scene arrays and its render workspace
+// (grown on demand). A device may appear more than once in rs_scene_commit_devices (virtual
+// devices, e.g. for tests): every replica owns its own stream and buffers.
+struct Replica {
     int device = 0;
+    hipStream_t stream = nullptr;           // the replica's own stream (multi-device renders)
+    DScene ds{};
+    std::vector<void*> dev;                 // scene allocations
+    double* d_rad = nullptr; size_t rad_cap = 0;
+    double* d_acc = nullptr; size_t acc_cap = 0;
+    unsigned long long* d_cnt = nullptr;
+    uint8_t* d_mask = nullptr; size_t mask_cap = 0;
+    float* d_out = nullptr; size_t out_cap = 0;
+    // wavefront path state (capacity wf_cap paths) + per-chunk queue counters
+    void* d_wf = nullptr; size_t wf_cap = 0;
+    uint32_t* d_counts = nullptr; size_t counts_cap = 0;
+    int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
+    uint32_t** d_qptrs = nullptr;                 // device array of the per-class queues
+    uint32_t* qptr[kWfsClasses] = {nullptr};
+    int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond kStackMax)
+
+    ~Replica() {
+        int prev = -1;
+        const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
+        for (void* p : dev) (void)hipFree(p);
+        for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts,
+                        (void*)d_ovf})
+            if (p) (void)hipFree(p);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (switched) (void)hipSetDevice(prev);
+    }
+};
+
+struct rs_scene {
     std::vector<rs_material_desc> mdesc;
     std::vector<HPerlin> perlins;
     std::vector<HImage> images;
@@ -160,42 +203,16 @@ struct rs_scene {
     bool spheres_only = false;
     int scene_mode = kSmGeneric;        // rs_internal.h SceneMode
     bool ref_order = false;                 // BVH::hit recursion order needed (non-monotone objects)
-    DScene ds{};
-    std::vector<void*> dev;                 // scene allocations
-    // render workspace (grown on demand, freed with the scene)
-    double* d_rad = nullptr; size_t rad_cap = 0;
-    double* d_acc = nullptr; size_t acc_cap = 0;
-    unsigned long long* d_cnt = nullptr;
-    uint8_t* d_mask = nullptr; size_t mask_cap = 0;
-    float* d_out = nullptr; size_t out_cap = 0;
-    // wavefront path state (capacity wf_cap paths) + per-chunk queue counters
-    void* d_wf = nullptr; size_t wf_cap = 0;
-    uint32_t* d_counts = nullptr; size_t counts_cap = 0;
+    HostScene hs;                           // device layout, built once by commit
+    std::vector<std::unique_ptr<Replica>> reps;   // the devices the scene is committed to, in call order
     uint64_t wf_chunk = 32ull << 20;              // RS_WF_CHUNK overrides
-    int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
-    uint32_t** d_qptrs = nullptr;                 // device array of the per-class queues
-    uint32_t* qptr[kWfsClasses] = {nullptr};
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
     uint64_t max_items_per_batch = 32ull << 20;  // RS_MAX_BATCH_ITEMS overrides (tests)
-    int tree_depth = 0;
+    int tree_depth = 0;                     // levels of the tree in use
+    int tree_arity = 0;                     // 4: 4-wide tree, 2: binary tree, 0: empty world
+    int stack_need = 0;                     // exact worst-case traversal stack depth of that tree
+    size_t n_nodes = 0;
     double time0 = 0.0, time1 = 0.0;        // World::new time_limit (world.rs:40-53)
-    std::vector<Box3> boxes;                // per-handle reference bbox (time range [0, 0])
-
-    ~rs_scene() { release(); }
-    void release() {
-        for (void* p : dev) (void)hipFree(p);
-        dev.clear();
-        if (d_rad) (void)hipFree(d_rad);
-        if (d_acc) (void)hipFree(d_acc);
-        if (d_cnt) (void)hipFree(d_cnt);
-        if (d_mask) (void)hipFree(d_mask);
-        if (d_out) (void)hipFree(d_out);
-        if (d_wf) (void)hipFree(d_wf);
-        if (d_counts) (void)hipFree(d_counts);
-        d_wf = nullptr; d_counts = nullptr; wf_cap = counts_cap = 0;
-        d_rad = d_acc = nullptr; d_cnt = nullptr; d_mask = nullptr; d_out = nullptr;
-        rad_cap = acc_cap = mask_cap = out_cap = 0;
-    }
 
     uint32_t add(HObj o) {
         if (committed) throw Error(RS_E_STATE, "scene already committed");
@@ -475,6 +492,32 @@ int32_t collapse4(const std::vector<HNode>& bn, int32_t code, std::vector<HNode4
     }
     return idx;
 }
+// Exact worst-case stack depth of traverse() (rs_kernels.hip) over a tree: the most entries any
+// root-to-node path can leave on the stack.
+//  4-wide near-first: a node pushes (inner children hit) - 1 <= (inner children) - 1 entries;
+int stack_need4(const std::vector<HNode4>& n4, int32_t code) {
+    if (code < 0) return 0;
+    int inner = 0, deepest = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int32_t c = n4[code].child[k];
+        if (c >= 0) { ++inner; deepest = std::max(deepest, stack_need4(n4, c)); }
+    }
+    return std::max(inner - 1, 0) + deepest;
+}
+//  binary near-first: one entry (the farther child) when both children are inner nodes;
+int stack_need2(const std::vector<HNode>& bn, int32_t code) {
+    if (code < 0) return 0;
+    const int32_t c0 = bn[code].child[0], c1 = bn[code].child[1];
+    const int a = stack_need2(bn, c0), b = stack_need2(bn, c1);
+    return (c0 >= 0 && c1 >= 0 ? 1 : 0) + std::max(a, b);
+}
+//  binary reference order: the node itself while its left (inner) subtree is searched.
+int stack_need_ref(const std::vector<HNode>& bn, int32_t code) {
+    if (code < 0) return 0;
+    const int32_t c0 = bn[code].child[0], c1 = bn[code].child[1];
+    return std::max(c0 >= 0 ? 1 + stack_need_ref(bn, c0) : 0, c1 >= 0 ? stack_need_ref(bn, c1) : 0);
+}
+
 DNode4 to_device4(const HNode4& h) {
     DNode4 d;
     std::memset(&d, 0, sizeof(d));
@@ -487,17 +530,41 @@ DNode4 to_device4(const HNode4& h) {
 }
 
 template <typename T>
-T* upload(rs_scene* s, const std::vector<T>& v) {
-    if (v.empty()) return nullptr;
-    void* p = nullptr;
-    HIP_OK(hipMalloc(&p, v.size() * sizeof(T)));
-    s->dev.push_back(p);
-    HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    return (T*)p;
+void stage(rs_scene* s, const T*& field, const std::vector<T>& v) {
+    field = nullptr;  // set per replica (upload_replica); an empty array stays null
+    if (v.empty()) return;
+    Blob b;
+    b.field_off = (size_t)((const char*)&field - (const char*)&s->hs.ds);
+    b.bytes.assign((const char*)v.data(), (const char*)v.data() + v.size() * sizeof(T));
+    s->hs.blobs.push_back(std::move(b));
 }
 
-void commit(rs_scene* s) {
+// copy the staged scene to `device` as a new replica
+void upload_replica(rs_scene* s, int device) {
+    std::unique_ptr<Replica> R(new Replica());
+    R->device = device;
+    HIP_OK(hipSetDevice(device));
+    R->ds = s->hs.ds;
+    for (const Blob& b : s->hs.blobs) {
+        void* p = nullptr;
+        HIP_OK(hipMalloc(&p, b.bytes.size()));
+        R->dev.push_back(p);
+        HIP_OK(hipMemcpy(p, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice));
+        std::memcpy((char*)&R->ds + b.field_off, &p, sizeof(void*));
+    }
+    HIP_OK(hipMalloc((void**)&R->d_cnt, 512 * sizeof(unsigned long long)));
+    HIP_OK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, device));
+    R->n_cu = prop.multiProcessorCount;
+    HIP_OK(wf_occupancy(s->scene_mode, &R->ext_bpc, &R->shade_bpc));
+    s->reps.push_back(std::move(R));
+}
+
+// Build the device layout of the scene on the host (BVH, flattened objects, materials, textures).
+void build(rs_scene* s) {
     if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+    s->hs = HostScene();
     for (uint32_t h : s->world) if (s->nest_depth(h) > RS_MAX_NEST) throw Error(RS_E_UNSUPPORTED, "object nesting deeper than the GPU path supports");
     for (uint32_t h : s->lights) if (s->nest_depth(h) > RS_MAX_NEST) throw Error(RS_E_UNSUPPORTED, "light nesting deeper than the GPU path supports");
 
@@ -541,7 +608,6 @@ void commit(rs_scene* s) {
     if (needs_lights && s->lights.empty())
         throw Error(RS_E_NO_LIGHTS, "scene has pdf materials but an empty lights list (reference: % 0 panic, list.rs:51)");
 
-    HIP_OK(hipGetDevice(&s->device));
     // flatten every handle
     std::vector<DPrim> prims(s->objs.size());
     std::vector<DSphere> spheres; std::vector<DRect> rects; std::vector<DBox> boxes; std::vector<DQuadric> quads;
@@ -672,11 +738,10 @@ void commit(rs_scene* s) {
             root = code;
         }
     }
-    if (B.max_depth > kStackMax) throw Error(RS_E_UNSUPPORTED, "BVH deeper than the traversal stack");
     s->tree_depth = B.max_depth;
 
     std::vector<int32_t> lights(s->lights.begin(), s->lights.end());
-    DScene& d = s->ds;
+    DScene& d = s->hs.ds;
     std::memset(&d, 0, sizeof(d));
     std::vector<DNode> dnodes;
     for (const HNode& h : B.nodes) dnodes.push_back(to_device(h));
@@ -703,40 +768,49 @@ void commit(rs_scene* s) {
         pclass[h] = (uint8_t)class_of((uint32_t)h);
         if (pclass[h] < kWfsClasses) s->class_mask |= 1u << pclass[h];
     }
-    d.nodes = upload(s, dnodes);
-    d.pbox = upload(s, pboxes);
-    d.pclass = upload(s, pclass);
+    stage(s, d.nodes, dnodes);
+    stage(s, d.pbox, pboxes);
+    stage(s, d.pclass, pclass);
     d.root4 = -1;
+    s->tree_arity = root >= 0 ? 2 : 0;
+    s->n_nodes = B.nodes.size();
+    if (root >= 0) s->stack_need = s->ref_order ? stack_need_ref(B.nodes, root) : stack_need2(B.nodes, root);
     if (!s->ref_order && root >= 0 && !std::getenv("RS_NO_BVH4")) {
         std::vector<HNode4> n4;
         int depth4 = 0;
         const int32_t r4 = collapse4(B.nodes, root, n4, 0, depth4);
-        if (r4 >= 0 && 3 * depth4 <= kStackMax) {
+        if (r4 >= 0) {
             std::vector<DNode4> dn4;
             for (const HNode4& h : n4) dn4.push_back(to_device4(h));
-            d.nodes4 = upload(s, dn4);
+            stage(s, d.nodes4, dn4);
             d.root4 = r4;
+            s->tree_arity = 4;
+            s->tree_depth = depth4;
+            s->n_nodes = n4.size();
+            s->stack_need = stack_need4(n4, r4);
         }
     }
-    d.prims = upload(s, prims);
-    d.spheres = upload(s, spheres);
+    d.stack_need = s->stack_need;
+    d.stk_ovf = nullptr;  // sized per launch grid (ensure_stack_overflow)
+    stage(s, d.prims, prims);
+    stage(s, d.spheres, spheres);
     if (s->spheres_only) {  // prim-indexed copy: the traversal's leaf test reads it without the DPrim hop
         std::vector<DSphere> psph(s->objs.size());
         std::memset(psph.data(), 0, psph.size() * sizeof(DSphere));
         for (size_t h = 0; h < s->objs.size(); ++h)
             if (s->objs[h].kind == PK_SPHERE) psph[h] = spheres[prims[h].idx];
-        d.psph = upload(s, psph);
+        stage(s, d.psph, psph);
     }
-    d.rects = upload(s, rects);
-    d.boxes = upload(s, boxes);
-    d.quadrics = upload(s, quads);
-    d.tris = upload(s, tris);
-    d.csgs = upload(s, csgs);
-    d.xforms = upload(s, xforms);
-    d.tf_fwd = upload(s, tf_f);
-    d.tf_inv = upload(s, tf_i);
-    d.mats = upload(s, mats);
-    d.media = upload(s, media);
+    stage(s, d.rects, rects);
+    stage(s, d.boxes, boxes);
+    stage(s, d.quadrics, quads);
+    stage(s, d.tris, tris);
+    stage(s, d.csgs, csgs);
+    stage(s, d.xforms, xforms);
+    stage(s, d.tf_fwd, tf_f);
+    stage(s, d.tf_inv, tf_i);
+    stage(s, d.mats, mats);
+    stage(s, d.media, media);
     d.has_media = media.empty() ? 0 : 1;
     // texture tables: Perlin values / permutations, image pixels
     std::vector<DPerlin> dper;
@@ -759,22 +833,59 @@ void commit(rs_scene* s) {
         tu8.insert(tu8.end(), hi.rgb.begin(), hi.rgb.end());
         dimg.push_back(x);
     }
-    d.perlins = upload(s, dper);
-    d.tex_f64 = upload(s, tf64);
-    d.tex_i32 = upload(s, ti32);
-    d.images = upload(s, dimg);
-    d.tex_u8 = upload(s, tu8);
+    stage(s, d.perlins, dper);
+    stage(s, d.tex_f64, tf64);
+    stage(s, d.tex_i32, ti32);
+    stage(s, d.images, dimg);
+    stage(s, d.tex_u8, tu8);
     d.uv = 0;  // only the Image texture reads (u, v)
     for (const DMaterial& m : mats) if (m.tex_kind == RS_TEX_IMAGE) d.uv = 1;
-    d.pad5 = 0;
-    d.lights = upload(s, lights);
+    stage(s, d.lights, lights);
     d.n_lights = (int32_t)lights.size();
     d.root = root;
     d.default_mat = default_mat;
     d.ref_order = s->ref_order ? 1 : 0;
     for (int i = 0; i < 3; ++i) { d.bg_lo[i] = s->bg_lo[i]; d.bg_hi[i] = s->bg_hi[i]; }
     d.bg_lo[3] = d.bg_hi[3] = 1.0f;
-    HIP_OK(hipMalloc((void**)&s->d_cnt, 512 * sizeof(unsigned long long)));
+}
+
+// rs_scene_commit / rs_scene_commit_devices: build once, then one replica per listed device
+// (none: a host-only build whose tree can be inspected with rs_scene_get_info).
+// devices == nullptr with n == 1: the current device (rs_scene_commit).
+void commit(rs_scene* s, const int* devices, int n) {
+    if (s->committed) throw Error(RS_E_STATE, "scene already committed");
+    if (n < 0 || (n > 1 && !devices)) throw Error(RS_E_INVALID, "bad device list");
+    build(s);  // scene errors (e.g. RS_E_NO_LIGHTS) before any device work
+    int current = 0;
+    if (n == 1 && !devices) {
+        HIP_OK(hipGetDevice(&current));
+        devices = &current;
+    }
+    int count = 0;
+    if (n > 0) HIP_OK(hipGetDeviceCount(&count));
+    for (int i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= count) throw Error(RS_E_INVALID, "device ordinal out of range");
+    int prev = 0;
+    if (n > 0) HIP_OK(hipGetDevice(&prev));
+    try {
+        for (int i = 0; i < n; ++i) upload_replica(s, devices[i]);
+        // peer access between distinct devices, for the frame-end row gather of rs_render_device
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                if (devices[i] == devices[j]) continue;
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, devices[i], devices[j]) == hipSuccess && can) {
+                    (void)hipSetDevice(devices[i]);
+                    (void)hipDeviceEnablePeerAccess(devices[j], 0);  // already enabled is fine
+                    (void)hipGetLastError();
+                }
+            }
+    } catch (...) {
+        s->reps.clear();
+        (void)hipSetDevice(prev);
+        throw;
+    }
+    if (n > 0) HIP_OK(hipSetDevice(prev));
     s->committed = true;
 }
 
@@ -830,17 +941,28 @@ void ensure(T*& p, size_t& cap, size_t n) {
     cap = n;
 }
 
-WfState carve_wf(rs_scene* s, uint64_t cap) {
+// Traversal-stack overflow for launches of at most `threads` grid threads: (stack_need - kStackMax)
+// entries per thread (DScene::stk_ovf). Nothing is allocated when the tree fits the LDS stack.
+void ensure_stack_overflow(const rs_scene* s, Replica& R, uint64_t threads) {
+    const int extra = s->stack_need - kStackMax;
+    if (extra <= 0) { R.ds.stk_ovf = nullptr; return; }
+    ensure(R.d_ovf, R.ovf_cap, (size_t)extra * threads);
+    R.ds.stk_ovf = R.d_ovf;
+}
+
+WfState carve_wf(Replica& R, uint64_t cap) {
     const size_t per_set = 3 * sizeof(D4) + sizeof(uint32_t);
     const size_t per = 2 * per_set + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
-    if (cap > s->wf_cap) {
-        if (s->d_wf) HIP_OK(hipFree(s->d_wf));
-        s->d_wf = nullptr;
-        HIP_OK(hipMalloc(&s->d_wf, per * cap + 8192));
-        s->wf_cap = cap;
+    const bool fresh = cap > R.wf_cap;
+    if (fresh) {
+        if (R.d_wf) HIP_OK(hipFree(R.d_wf));
+        R.d_wf = nullptr;
+        R.wf_cap = 0;
+        HIP_OK(hipMalloc(&R.d_wf, per * cap + 8192));
+        R.wf_cap = cap;
     }
-    char* p = (char*)s->d_wf;
-    const uint64_t c = s->wf_cap;
+    char* p = (char*)R.d_wf;
+    const uint64_t c = R.wf_cap;
     WfState w;
     for (int k = 0; k < 2; ++k) {
         WfSet& t = w.set[k];
@@ -854,9 +976,9 @@ WfState carve_wf(rs_scene* s, uint64_t cap) {
     uint32_t* qp[kWfsClasses];
     for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p += sizeof(uint32_t) * c; }
     p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
-    s->d_qptrs = (uint32_t**)p;
-    HIP_OK(hipMemcpy(s->d_qptrs, qp, sizeof(qp), hipMemcpyHostToDevice));
-    for (int k = 0; k < kWfsClasses; ++k) s->qptr[k] = qp[k];
+    R.d_qptrs = (uint32_t**)p;
+    if (fresh) HIP_OK(hipMemcpy(R.d_qptrs, qp, sizeof(qp), hipMemcpyHostToDevice));
+    for (int k = 0; k < kWfsClasses; ++k) R.qptr[k] = qp[k];
     w.counts = nullptr;
     w.cap = (uint32_t)c;
     return w;
@@ -871,36 +993,82 @@ struct DeviceGuard {
     ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
-void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* d_mask,
-                   float* d_out, hipStream_t stream, rs_render_stats* stats) {
-    if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
-    if (!cam || !st || !d_out) throw Error(RS_E_INVALID, "null argument");
-    if (cam->width == 0 || cam->height == 0) throw Error(RS_E_INVALID, "empty image");
-    if (st->mode < RS_MODE_AUTO || st->mode > RS_MODE_WAVEFRONT) throw Error(RS_E_INVALID, "unknown render mode");
-    const bool wavefront = st->mode != RS_MODE_MEGAKERNEL;
-    const uint32_t W = cam->width, H = cam->height;
-    const uint32_t rb = st->row_begin;
+// Rows of the call's lattice (row_begin, row_end, row_step) that replica k of n renders: every n-th
+// lattice row starting at the k-th, the interleave of render_rows (painter.rs:248) over devices.
+struct RowSet {
+    uint32_t begin = 0, end = 0, step = 1;
+    uint32_t count() const { return begin < end ? (end - begin + step - 1) / step : 0; }
+};
+RowSet replica_rows(const rs_camera_desc* cam, const rs_render_settings* st, uint32_t k, uint32_t n) {
+    RowSet r;
+    const uint32_t H = cam->height;
     const uint32_t re = st->row_end ? std::min(st->row_end, H) : H;
     const uint32_t rstep = st->row_step ? st->row_step : 1;
-    if (rb >= re) { if (stats) *stats = rs_render_stats{0, 0, 0.0, 0.0, 0, 0, 0.0, 0, 0, 0}; return; }
-    const uint32_t n_rows = (re - rb + rstep - 1) / rstep;
-    const uint64_t n_pix64 = (uint64_t)n_rows * W;
-    if (n_pix64 > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "frame too large");
-    const uint32_t n_pix = (uint32_t)n_pix64;
+    const uint64_t b = (uint64_t)st->row_begin + (uint64_t)k * rstep;
+    r.end = re;
+    r.begin = b < re ? (uint32_t)b : re;
+    r.step = (uint32_t)std::min<uint64_t>((uint64_t)rstep * n, 0xFFFFFFFFull);
+    return r;
+}
+
+// One replica's share of a frame between enqueue and finish: multi-device renders enqueue every
+// replica before waiting for any, so the devices run concurrently.
+struct Pending {
+    Replica* R = nullptr;
+    hipStream_t stream = nullptr;
+    bool empty = true;
+    bool wavefront = false, sorted = false;
+    uint32_t n_pix = 0, N = 0, depth = 0, n_batches = 0, path_launches = 0;
+    uint64_t n_chunks_total = 0;
+    size_t ki = 0;
+    std::vector<hipEvent_t> ev, kev;
+    unsigned long long cnt[512];
+    std::vector<uint32_t> qc;
+    ~Pending() {
+        for (auto& e : ev) (void)hipEventDestroy(e);
+        for (auto& e : kev) (void)hipEventDestroy(e);
+    }
+};
+
+void validate_render(const rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st) {
+    if (!cam || !st) throw Error(RS_E_INVALID, "null argument");
+    if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
+    if (s->reps.empty()) throw Error(RS_E_STATE, "scene committed without devices (host-only build)");
+    if (cam->width == 0 || cam->height == 0) throw Error(RS_E_INVALID, "empty image");
+    if (st->mode < RS_MODE_AUTO || st->mode > RS_MODE_WAVEFRONT) throw Error(RS_E_INVALID, "unknown render mode");
+    const uint32_t re = st->row_end ? std::min(st->row_end, cam->height) : cam->height;
+    const uint32_t rstep = st->row_step ? st->row_step : 1;
+    if (st->row_begin < re && (uint64_t)((re - st->row_begin + rstep - 1) / rstep) * cam->width > 0xFFFFFFFFull)
+        throw Error(RS_E_INVALID, "frame too large");
+}
+
+// Enqueue the rows `rows` of the frame on replica R (its device must be current): batches of camera
+// samples -> wavefront or megakernel -> ordered accumulation -> into_color into d_out (W*H RGBA on
+// R's device). Nothing here waits for the device.
+void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, const rs_render_settings* st,
+                    RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t stream, Pending& P) {
+    P.R = &R;
+    P.stream = stream;
+    const bool wavefront = st->mode != RS_MODE_MEGAKERNEL;
+    const uint32_t W = cam->width, H = cam->height;
+    const uint32_t n_rows = rows.count();
+    if (n_rows == 0) return;
+    P.empty = false;
+    const uint32_t n_pix = (uint32_t)((uint64_t)n_rows * W);
     const uint32_t sq = (uint32_t)std::floor(std::sqrt((double)st->samples));  // painter.rs:110-118
     const uint32_t N = sq * sq;
 
     DCamera dc = make_camera(*cam);
     PathParams pp;
-    pp.n_pix_local = n_pix; pp.width = W; pp.height = H; pp.row_begin = rb; pp.row_step = rstep;
+    pp.n_pix_local = n_pix; pp.width = W; pp.height = H; pp.row_begin = rows.begin; pp.row_step = rows.step;
     pp.sqrt_spp = sq; pp.depth = st->depth;
     pp.key_base = splitmix64_h(splitmix64_h(st->seed) ^ (uint64_t)st->pass);
     pp.mask = d_mask;
 
     uint32_t spb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(N, s->max_items_per_batch / n_pix));
     if (N == 0) spb = 0;
-    ensure(s->d_acc, s->acc_cap, (size_t)3 * n_pix);
-    if (spb) ensure(s->d_rad, s->rad_cap, (size_t)3 * n_pix * spb);
+    ensure(R.d_acc, R.acc_cap, (size_t)3 * n_pix);
+    if (spb) ensure(R.d_rad, R.rad_cap, (size_t)3 * n_pix * spb);
 
     const uint32_t n_batches = spb ? (N + spb - 1) / spb : 0;
     const uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(s->wf_chunk, (uint64_t)n_pix * std::max(spb, 1u)));
@@ -914,154 +1082,277 @@ void render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
                                       s->scene_mode == kSmNest2);
     const uint32_t cstride = sorted ? kWfsStride : 1;
     if (wavefront && N > 0) {
-        WS = carve_wf(s, chunk);
+        WS = carve_wf(R, chunk);
         const size_t nc = (size_t)n_chunks_total * (st->depth + 1) * cstride;
-        ensure(s->d_counts, s->counts_cap, nc);
-        WS.counts = s->d_counts;
-        if (!s->n_cu) {
-            hipDeviceProp_t prop;
-            HIP_OK(hipGetDeviceProperties(&prop, s->device));
-            s->n_cu = prop.multiProcessorCount;
-            HIP_OK(wf_occupancy(s->scene_mode, &s->ext_bpc, &s->shade_bpc));
-        }
+        ensure(R.d_counts, R.counts_cap, nc);
+        WS.counts = R.d_counts;
     }
+    // launch grids: grid-stride kernels over at most these many blocks
+    const uint32_t ext_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.ext_bpc));
+    const uint32_t shade_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.shade_bpc));
+    const uint32_t wide = (uint32_t)std::max(1, R.n_cu * 8);
+    const uint32_t mega_blocks = wide;
+    ensure_stack_overflow(s, R, (uint64_t)std::max(std::max(ext_blocks, shade_blocks), wide) * kBlock);
     const size_t n_kernel_ev = wavefront ? (size_t)n_chunks_total * st->depth : n_batches;
-    std::vector<hipEvent_t> ev(2 * (size_t)n_batches), kev(2 * n_kernel_ev);
-    for (auto& e : ev) HIP_OK(hipEventCreate(&e));
-    for (auto& e : kev) HIP_OK(hipEventCreate(&e));
-    auto t0 = std::chrono::steady_clock::now();
-    HIP_OK(hipMemsetAsync(s->d_cnt, 0, 512 * sizeof(unsigned long long), stream));
+    P.ev.assign(2 * (size_t)n_batches, nullptr);
+    P.kev.assign(2 * n_kernel_ev, nullptr);
+    for (auto& e : P.ev) HIP_OK(hipEventCreate(&e));
+    for (auto& e : P.kev) HIP_OK(hipEventCreate(&e));
+    const DScene& ds = R.ds;
+    HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
     if (wavefront && N > 0)
-        HIP_OK(hipMemsetAsync(s->d_counts, 0, (size_t)n_chunks_total * (st->depth + 1) * cstride * sizeof(uint32_t), stream));
-    if (N == 0) HIP_OK(hipMemsetAsync(s->d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
+        HIP_OK(hipMemsetAsync(R.d_counts, 0, (size_t)n_chunks_total * (st->depth + 1) * cstride * sizeof(uint32_t), stream));
+    if (N == 0) HIP_OK(hipMemsetAsync(R.d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
     uint32_t bi = 0;
     size_t ki = 0;
     uint64_t chunk_i = 0;
     uint32_t path_launches = 0;
-    const uint32_t ext_blocks = (uint32_t)std::max(1, s->n_cu * std::max(1, s->ext_bpc));
-    const uint32_t shade_blocks = (uint32_t)std::max(1, s->n_cu * std::max(1, s->shade_bpc));
     for (uint32_t s0 = 0; s0 < N; s0 += spb, ++bi) {
         const uint32_t nb = std::min(spb, N - s0);
         pp.s0 = s0;
         pp.n_items = (uint64_t)n_pix * nb;
-        HIP_OK(hipEventRecord(ev[2 * bi], stream));
+        HIP_OK(hipEventRecord(P.ev[2 * bi], stream));
         if (!wavefront) {
-            HIP_OK(hipEventRecord(kev[2 * ki], stream));
-            HIP_OK(launch_path_mega(s->ds, dc, pp, s->scene_mode, s->d_rad, s->d_cnt, stream));
-            HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
+            HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
+            HIP_OK(launch_path_mega(ds, dc, pp, s->scene_mode, R.d_rad, R.d_cnt, mega_blocks, stream));
+            HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
             ++ki;
             ++path_launches;
         } else {
             for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i) {
                 const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, pp.n_items - c0);
-                WS.counts = s->d_counts + chunk_i * (st->depth + 1) * cstride;
+                WS.counts = R.d_counts + chunk_i * (st->depth + 1) * cstride;
                 if (!sorted) {  // the sorted path generates camera rays inside its bounce-0 extend
-                    HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, s->d_rad, stream));
+                    HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, R.d_rad, stream));
                     ++path_launches;
                 }
-                const uint32_t wide = (uint32_t)(s->n_cu * 8);
                 for (uint32_t b = 0; sorted && b < st->depth; ++b) {
-                    HIP_OK(hipEventRecord(kev[2 * ki], stream));
+                    HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
                     if (b == 0)
-                        HIP_OK(launch_wfs_gen_extend(s->ds, dc, pp, WS, s->d_qptrs, cstride, c0, n, s->d_rad,
+                        HIP_OK(launch_wfs_gen_extend(ds, dc, pp, WS, R.d_qptrs, cstride, c0, n, R.d_rad,
                                                      std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     else
-                        HIP_OK(launch_wfs_extend(s->ds, WS, s->d_qptrs, b, cstride, pp.n_items, s->d_rad,
+                        HIP_OK(launch_wfs_extend(ds, WS, R.d_qptrs, b, cstride, pp.n_items, R.d_rad,
                                                  std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
-                    HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
+                    HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
                     ++ki;
                     ++path_launches;
                     for (int k = 0; k < kWfsClasses; ++k) {
                         if (!(s->class_mask & (1u << k))) continue;  // no prim of this class: empty queue
-                        HIP_OK(launch_wfs_shade(s->ds, WS, s->qptr[k], k, b, cstride, st->depth, pp.n_items, s->d_rad,
+                        HIP_OK(launch_wfs_shade(ds, WS, R.qptr[k], k, b, cstride, st->depth, pp.n_items, R.d_rad,
                                                 std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                         ++path_launches;
                     }
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
-                    HIP_OK(hipEventRecord(kev[2 * ki], stream));
-                    HIP_OK(launch_wf_extend(s->ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
-                    HIP_OK(hipEventRecord(kev[2 * ki + 1], stream));
+                    HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
+                    HIP_OK(launch_wf_extend(ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
+                    HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
                     ++ki;
-                    HIP_OK(launch_wf_shade(s->ds, WS, b, st->depth, pp.n_items, s->d_rad,
+                    HIP_OK(launch_wf_shade(ds, WS, b, st->depth, pp.n_items, R.d_rad,
                                            std::min(shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     path_launches += 2;
                 }
             }
         }
-        HIP_OK(hipEventRecord(ev[2 * bi + 1], stream));
-        HIP_OK(launch_accumulate(s->d_rad, s->d_acc, n_pix, nb, s0 == 0, stream));
+        HIP_OK(hipEventRecord(P.ev[2 * bi + 1], stream));
+        HIP_OK(launch_accumulate(R.d_rad, R.d_acc, n_pix, nb, s0 == 0, stream));
     }
     FinalParams fp;
-    fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rb; fp.row_step = rstep; fp.n_samples = N;
+    fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rows.begin; fp.row_step = rows.step; fp.n_samples = N;
     fp.gamma = st->gamma; fp.mask = d_mask;
-    HIP_OK(launch_finalize(s->d_acc, d_out, fp, stream));
-    unsigned long long cnt[512];
-    HIP_OK(hipMemcpyAsync(cnt, s->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, stream));
-    const uint32_t cstride_f = sorted ? kWfsStride : 1;
-    std::vector<uint32_t> qc(wavefront && N > 0 ? (size_t)n_chunks_total * (st->depth + 1) * cstride_f : 0);
-    if (!qc.empty()) HIP_OK(hipMemcpyAsync(qc.data(), s->d_counts, qc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipStreamSynchronize(stream));
-    auto t1 = std::chrono::steady_clock::now();
+    HIP_OK(launch_finalize(R.d_acc, d_out, fp, stream));
+    P.wavefront = wavefront;
+    P.sorted = sorted;
+    P.n_pix = n_pix;
+    P.N = N;
+    P.depth = st->depth;
+    P.n_batches = n_batches;
+    P.n_chunks_total = n_chunks_total;
+    P.ki = ki;
+    P.path_launches = path_launches;
+}
+
+// Wait for replica P's share and add its statistics into *stats (which the caller zeroed).
+void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
+    if (P.empty) return;
+    Replica& R = *P.R;
+    HIP_OK(hipMemcpyAsync(P.cnt, R.d_cnt, sizeof(P.cnt), hipMemcpyDeviceToHost, P.stream));
+    const uint32_t cstride_f = P.sorted ? kWfsStride : 1;
+    P.qc.assign(P.wavefront && P.N > 0 ? (size_t)P.n_chunks_total * (P.depth + 1) * cstride_f : 0, 0u);
+    if (!P.qc.empty())
+        HIP_OK(hipMemcpyAsync(P.qc.data(), R.d_counts, P.qc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, P.stream));
+    HIP_OK(hipStreamSynchronize(P.stream));
+    if (!stats) return;
     double path_ms = 0.0;
-    for (uint32_t b = 0; b < n_batches; ++b) {
+    for (uint32_t b = 0; b < P.n_batches; ++b) {
         float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, ev[2 * b], ev[2 * b + 1]));
+        HIP_OK(hipEventElapsedTime(&ms, P.ev[2 * b], P.ev[2 * b + 1]));
         path_ms += ms;
     }
     double kernel_ms = 0.0;
-    for (size_t k = 0; k < ki; ++k) {
+    for (size_t k = 0; k < P.ki; ++k) {
         float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, kev[2 * k], kev[2 * k + 1]));
+        HIP_OK(hipEventElapsedTime(&ms, P.kev[2 * k], P.kev[2 * k + 1]));
         kernel_ms += ms;
     }
-    for (auto& e : ev) (void)hipEventDestroy(e);
-    for (auto& e : kev) (void)hipEventDestroy(e);
-    if (stats) {
-        stats->path_ms = path_ms;
-        stats->launches = path_launches;
-        stats->kernel_launches = (uint32_t)ki;
-        stats->kernel_ms = kernel_ms;
-        uint64_t seg = 0;
-        for (int i = 0; i < 256; ++i) seg += cnt[i];
-        uint64_t cont = 0, seg0 = 0, cont0 = 0;
-        if (!qc.empty()) {  // segments = sum over bounces of the extend queue lengths
-            seg = 0;
-            for (uint64_t c = 0; c < n_chunks_total; ++c)
-                for (uint32_t b = 0; b < st->depth; ++b) {
-                    const uint32_t* q = &qc[(c * (st->depth + 1) + b) * cstride_f];
-                    uint64_t cb = 0;
-                    if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cb += q[1 + k];
-                    if (b == 0) { seg0 += q[0]; cont0 += cb; }
-                    seg += q[0];
-                    cont += cb;
-                }
-        }
-        // algorithmic bytes of the dominant kernel (DESIGN.md Roofline):
-        //  megakernel   : radiance out, 3 x f64 per sample
-        //  wf extend    : ray in (2 x 32 B records) + hit out (16 B) per segment
-        //  wfs extend   : bounces >= 1: ray in (64 B) per segment; + hit (16 B) + queue slot (4 B)
-        //                 per shaded segment; + throughput record in (32 B), item (4 B) and
-        //                 radiance out (24 B) per path ending in extend (sky miss / light hit).
-        //                 bounce 0 (fused with ray generation): radiance out (24 B) per sample that
-        //                 ends there (incl. masked); hit + queue slot + ray records (64 B, rng
-        //                 inside) + throughput record (32 B) + item (4 B) per shaded one
-        if (!wavefront) {
-            stats->kernel_id = RS_KERNEL_PATH_MEGA;
-            stats->kernel_bytes = 24ull * (uint64_t)n_pix * N;
-        } else if (cstride_f > 1) {
-            stats->kernel_id = RS_KERNEL_WFS_EXTEND;
-            const uint64_t items = (uint64_t)n_pix * N, segr = seg - seg0, contr = cont - cont0;
-            stats->kernel_bytes = 24ull * (items - cont0) + 120ull * cont0 +
-                                  64ull * segr + 20ull * contr + 60ull * (segr - contr);
-        } else {
-            stats->kernel_id = RS_KERNEL_WF_EXTEND;
-            stats->kernel_bytes = 80ull * seg;
-        }
-        stats->segments = seg;
-        stats->samples = (uint64_t)n_pix * N;  // masked-out pixels included (they trace nothing)
-        stats->ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    uint64_t seg = 0;
+    for (int i = 0; i < 256; ++i) seg += P.cnt[i];
+    uint64_t cont = 0, seg0 = 0, cont0 = 0;
+    if (!P.qc.empty()) {  // segments = sum over bounces of the extend queue lengths
+        seg = 0;
+        for (uint64_t c = 0; c < P.n_chunks_total; ++c)
+            for (uint32_t b = 0; b < P.depth; ++b) {
+                const uint32_t* q = &P.qc[(c * (P.depth + 1) + b) * cstride_f];
+                uint64_t cb = 0;
+                if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cb += q[1 + k];
+                if (b == 0) { seg0 += q[0]; cont0 += cb; }
+                seg += q[0];
+                cont += cb;
+            }
     }
+    // algorithmic bytes of the dominant kernel (DESIGN.md Roofline):
+    //  megakernel   : radiance out, 3 x f64 per sample
+    //  wf extend    : ray in (2 x 32 B records) + hit out (16 B) per segment
+    //  wfs extend   : bounces >= 1: ray in (64 B) per segment; + hit (16 B) + queue slot (4 B)
+    //                 per shaded segment; + throughput record in (32 B), item (4 B) and
+    //                 radiance out (24 B) per path ending in extend (sky miss / light hit).
+    //                 bounce 0 (fused with ray generation): radiance out (24 B) per sample that
+    //                 ends there (incl. masked); hit + queue slot + ray records (64 B, rng
+    //                 inside) + throughput record (32 B) + item (4 B) per shaded one
+    const uint64_t items = (uint64_t)P.n_pix * P.N;
+    uint64_t kbytes;
+    if (!P.wavefront) {
+        stats->kernel_id = RS_KERNEL_PATH_MEGA;
+        kbytes = 24ull * items;
+    } else if (cstride_f > 1) {
+        stats->kernel_id = RS_KERNEL_WFS_EXTEND;
+        const uint64_t segr = seg - seg0, contr = cont - cont0;
+        kbytes = 24ull * (items - cont0) + 120ull * cont0 + 64ull * segr + 20ull * contr + 60ull * (segr - contr);
+    } else {
+        stats->kernel_id = RS_KERNEL_WF_EXTEND;
+        kbytes = 80ull * seg;
+    }
+    stats->path_ms += path_ms;
+    stats->launches += P.path_launches;
+    stats->kernel_launches += (uint32_t)P.ki;
+    stats->kernel_ms += kernel_ms;
+    stats->kernel_bytes += kbytes;
+    stats->segments += seg;
+    stats->tree_arity = s->tree_arity;
+    stats->samples += items;  // masked-out pixels included (they trace nothing)
+}
+
+// copy rows `rows` of a W-wide RGBA f32 frame between two buffers of the same layout
+hipError_t copy_rows(float* dst, const float* src, uint32_t W, RowSet rows, hipMemcpyKind kind, hipStream_t st) {
+    const uint32_t n = rows.count();
+    if (n == 0) return hipSuccess;
+    const size_t row_bytes = (size_t)W * 4 * sizeof(float);
+    const size_t off = (size_t)rows.begin * W * 4;
+    return hipMemcpy2DAsync(dst + off, row_bytes * rows.step, src + off, row_bytes * rows.step, row_bytes, n, kind, st);
+}
+
+// rs_render_device: replica 0 renders its rows straight into d_out on the caller's stream; every
+// other replica renders into its own frame on its own stream and copies its rows into d_out.
+void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* d_mask,
+                         float* d_out, hipStream_t stream, rs_render_stats* stats) {
+    if (!d_out) throw Error(RS_E_INVALID, "null argument");
+    validate_render(s, cam, st);
+    rs_render_stats acc{};
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t n = (uint32_t)s->reps.size();
+    const size_t npx = (size_t)cam->width * cam->height;
+    std::vector<std::unique_ptr<Pending>> P(n);
+    std::vector<hipEvent_t> done(n, nullptr);
+    try {
+        for (uint32_t k = 0; k < n; ++k) {
+            Replica& R = *s->reps[k];
+            P[k].reset(new Pending());
+            const RowSet rows = replica_rows(cam, st, k, n);
+            DeviceGuard g(R.device);
+            if (k == 0) {
+                render_enqueue(s, R, cam, st, rows, d_mask, d_out, stream, *P[k]);
+                continue;
+            }
+            if (rows.count() == 0) continue;
+            ensure(R.d_out, R.out_cap, npx * 4);
+            const uint8_t* m = nullptr;
+            if (d_mask) {
+                ensure(R.d_mask, R.mask_cap, npx);
+                HIP_OK(hipMemcpyAsync(R.d_mask, d_mask, npx, hipMemcpyDefault, R.stream));
+                m = R.d_mask;
+            }
+            render_enqueue(s, R, cam, st, rows, m, R.d_out, R.stream, *P[k]);
+            HIP_OK(copy_rows(d_out, R.d_out, cam->width, rows, hipMemcpyDefault, R.stream));
+            HIP_OK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+            HIP_OK(hipEventRecord(done[k], R.stream));
+        }
+        {
+            DeviceGuard g(s->reps[0]->device);
+            for (uint32_t k = 1; k < n; ++k)
+                if (done[k]) HIP_OK(hipStreamWaitEvent(stream, done[k], 0));
+        }
+        for (uint32_t k = 0; k < n; ++k) {
+            DeviceGuard g(s->reps[k]->device);
+            render_finish(s, *P[k], &acc);
+        }
+        DeviceGuard g(s->reps[0]->device);
+        HIP_OK(hipStreamSynchronize(stream));
+    } catch (...) {
+        for (uint32_t k = 0; k < n; ++k)  // drain what was enqueued before the buffers go away
+            if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipStreamSynchronize(P[k]->stream); }
+        for (hipEvent_t e : done) if (e) (void)hipEventDestroy(e);
+        throw;
+    }
+    for (hipEvent_t e : done) if (e) (void)hipEventDestroy(e);
+    acc.tree_arity = s->tree_arity;
+    acc.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = acc;
+}
+
+// rs_render: every replica renders its rows into its own device frame on its own stream; the rows
+// are copied back into the caller's buffer (rows outside the call's lattice keep their values).
+void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask,
+                       float* out, rs_render_stats* stats) {
+    if (!out) throw Error(RS_E_INVALID, "null argument");
+    validate_render(s, cam, st);
+    rs_render_stats acc{};
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t n = (uint32_t)s->reps.size();
+    const size_t npx = (size_t)cam->width * cam->height;
+    std::vector<std::unique_ptr<Pending>> P(n);
+    std::vector<RowSet> rows(n);
+    try {
+        for (uint32_t k = 0; k < n; ++k) {
+            Replica& R = *s->reps[k];
+            P[k].reset(new Pending());
+            rows[k] = replica_rows(cam, st, k, n);
+            if (rows[k].count() == 0) continue;
+            DeviceGuard g(R.device);
+            ensure(R.d_out, R.out_cap, npx * 4);
+            const uint8_t* m = nullptr;
+            if (mask) {
+                ensure(R.d_mask, R.mask_cap, npx);
+                HIP_OK(hipMemcpyAsync(R.d_mask, mask, npx, hipMemcpyHostToDevice, R.stream));
+                m = R.d_mask;
+            }
+            render_enqueue(s, R, cam, st, rows[k], m, R.d_out, R.stream, *P[k]);
+        }
+        for (uint32_t k = 0; k < n; ++k) {
+            if (rows[k].count() == 0) continue;
+            Replica& R = *s->reps[k];
+            DeviceGuard g(R.device);
+            HIP_OK(copy_rows(out, R.d_out, cam->width, rows[k], hipMemcpyDeviceToHost, R.stream));
+            render_finish(s, *P[k], &acc);
+        }
+    } catch (...) {
+        for (uint32_t k = 0; k < n; ++k)
+            if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipStreamSynchronize(P[k]->stream); }
+        throw;
+    }
+    acc.tree_arity = s->tree_arity;
+    acc.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = acc;
 }
 
 }  // namespace
@@ -1304,16 +1595,38 @@ int rs_set_time_range(rs_scene* s, double t0, double t1) {
     });
 }
 int rs_scene_commit(rs_scene* s) {
-    return run([&] { commit(S(s)); });
+    return run([&] {
+        commit(S(s), nullptr, 1);
+    });
+}
+int rs_scene_commit_devices(rs_scene* s, const int* devices, int n) {
+    return run([&] {
+        if (n < 0 || (n > 0 && !devices)) throw Error(RS_E_INVALID, "bad device list");
+        commit(S(s), devices, n);
+    });
+}
+int rs_scene_get_info(const rs_scene* s, rs_scene_info* out) {
+    return run([&] {
+        if (!s || !out) throw Error(RS_E_INVALID, "null argument");
+        if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
+        std::memset(out, 0, sizeof(*out));
+        out->tree_arity = s->tree_arity;
+        out->ref_order = s->ref_order ? 1 : 0;
+        out->scene_mode = s->scene_mode;
+        out->tree_depth = s->tree_depth;
+        out->stack_need = s->stack_need;
+        out->stack_lds = kStackMax;
+        out->n_nodes = s->n_nodes;
+        out->n_objects = s->objs.size();
+        out->n_world = s->world.size();
+        out->n_devices = (int32_t)s->reps.size();
+    });
 }
 
 int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* d_mask,
                      float* d_out, void* stream, rs_render_stats* stats) {
     return run([&] {
-        S(s);
-        if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
-        DeviceGuard g(s->device);
-        render_device(s, cam, st, d_mask, d_out, (hipStream_t)stream, stats);
+        render_frame_device(S(s), cam, st, d_mask, d_out, (hipStream_t)stream, stats);
     });
 }
 
@@ -1382,12 +1695,15 @@ int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin,
         S(s);
         if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
         if (!rays || !out) throw Error(RS_E_INVALID, "null argument");
-        DeviceGuard g(s->device);
+        if (s->reps.empty()) throw Error(RS_E_STATE, "scene committed without devices (host-only build)");
+        Replica& R = *s->reps[0];
+        DeviceGuard g(R.device);
         double *dr = nullptr, *dout = nullptr;
         HIP_OK(hipMalloc((void**)&dr, (size_t)n * 7 * sizeof(double) + 8));
         HIP_OK(hipMalloc((void**)&dout, (size_t)n * 13 * sizeof(double) + 8));
         HIP_OK(hipMemcpy(dr, rays, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice));
-        HIP_OK(launch_probe_hit(s->ds, dr, n, tmin, tmax, dout, nullptr));
+        ensure_stack_overflow(s, R, ((uint64_t)n + kBlock - 1) / kBlock * kBlock);
+        HIP_OK(launch_probe_hit(R.ds, dr, n, tmin, tmax, dout, nullptr));
         HIP_OK(hipMemcpy(out, dout, (size_t)n * 13 * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(dr);
         (void)hipFree(dout);
@@ -1403,14 +1719,17 @@ int rs_probe_samples(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
         if (x >= cam->width || y >= cam->height) throw Error(RS_E_INVALID, "pixel outside the frame");
         const uint32_t sq = (uint32_t)std::floor(std::sqrt((double)st->samples));
         if ((uint64_t)s0 + n > (uint64_t)sq * sq) throw Error(RS_E_INVALID, "sample index beyond floor(sqrt(samples))^2");
-        DeviceGuard g(s->device);
+        if (s->reps.empty()) throw Error(RS_E_STATE, "scene committed without devices (host-only build)");
+        Replica& R = *s->reps[0];
+        DeviceGuard g(R.device);
         PathParams pp{};
         pp.n_pix_local = cam->width * cam->height; pp.width = cam->width; pp.height = cam->height;
         pp.row_begin = 0; pp.row_step = 1; pp.sqrt_spp = sq; pp.depth = st->depth;
         pp.key_base = splitmix64_h(splitmix64_h(st->seed) ^ (uint64_t)st->pass);
         double* dout = nullptr;
         HIP_OK(hipMalloc((void**)&dout, (size_t)n * 4 * sizeof(double) + 8));
-        HIP_OK(launch_probe_sample(s->ds, make_camera(*cam), pp, s->scene_mode, x, y, s0, n, dout, nullptr));
+        ensure_stack_overflow(s, R, ((uint64_t)n + kBlock - 1) / kBlock * kBlock);
+        HIP_OK(launch_probe_sample(R.ds, make_camera(*cam), pp, s->scene_mode, x, y, s0, n, dout, nullptr));
         HIP_OK(hipMemcpy(out, dout, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(dout);
     });
@@ -1419,22 +1738,7 @@ int rs_probe_samples(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
 int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask, float* out,
               rs_render_stats* stats) {
     return run([&] {
-        S(s);
-        if (!cam || !out) throw Error(RS_E_INVALID, "null argument");
-        if (!s->committed) throw Error(RS_E_STATE, "scene not committed");
-        DeviceGuard g(s->device);
-        const size_t npx = (size_t)cam->width * cam->height;
-        ensure(s->d_out, s->out_cap, npx * 4);
-        // rows not rendered keep the caller's values: seed the device frame with them
-        HIP_OK(hipMemcpy(s->d_out, out, npx * 4 * sizeof(float), hipMemcpyHostToDevice));
-        const uint8_t* dm = nullptr;
-        if (mask) {
-            ensure(s->d_mask, s->mask_cap, npx);
-            HIP_OK(hipMemcpy(s->d_mask, mask, npx, hipMemcpyHostToDevice));
-            dm = s->d_mask;
-        }
-        render_device(s, cam, st, dm, s->d_out, nullptr, stats);
-        HIP_OK(hipMemcpy(out, s->d_out, npx * 4 * sizeof(float), hipMemcpyDeviceToHost));
+        render_frame_host(S(s), cam, st, mask, out, stats);
     });
 }
 

@@ -7,7 +7,9 @@
 namespace rs {
 
 constexpr int kBlock = 256;      // 4 waves of 64
-constexpr int kStackMax = 24;    // per-thread BVH stack entries (LDS, 24 KiB/block -> 6 blocks/CU); host enforces tree depth
+// per-thread BVH stack entries held in LDS (24 KiB/block -> 6 blocks/CU); deeper entries spill to
+// DScene::stk_ovf, which the host sizes from the tree's exact worst-case stack depth
+constexpr int kStackMax = 24;
 
 // One batch of camera samples: items = n_pix_local * n_samp_batch, item -> (sample, pixel).
 // Scene modes (a template parameter of every path kernel): kSmSpheres -- world and lights are
@@ -63,11 +65,12 @@ struct FinalParams {
     const uint8_t* mask;
 };
 
-// Megakernel: one thread per (pixel, sample) path; radiance -> rad[c * n_items + item].
+// Megakernel: one thread per (pixel, sample) path (grid-stride over at most max_blocks blocks);
+// radiance -> rad[c * n_items + item].
 hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
                                uint32_t s0, uint32_t n, double* out, hipStream_t st);
 hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, int sm, double* rad,
-                            unsigned long long* seg_counters, hipStream_t st);
+                            unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st);
 hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
                          hipStream_t st);
 hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);

@@ -248,7 +248,30 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, 
 //    updated range -- needed for Box / Quadric / CSG, whose records depend on the range end.
 //    Each child box is tested when the recursion would visit it (the deferred right child is
 //    re-read from its parent when popped), so the tests see the same range as BVH::hit.
-// stk: this thread's column of the block's LDS stack (stride kBlock).
+// Traversal stack of one thread: entries [0, kStackMax) in its column of the block's LDS stack
+// (stride kBlock), deeper ones in its column of the HBM overflow array (stride = grid threads).
+// The host sizes the overflow from the tree's exact worst-case depth, so any tree depth works;
+// scenes whose trees fit the LDS part never touch HBM (the bound test is one compare per push/pop).
+struct Stk {
+    int* lds;
+    int* ovf;
+    uint32_t ostride;
+    __device__ __forceinline__ void put(int i, int v) const {
+        if (i < kStackMax) lds[i * kBlock] = v;
+        else ovf[(size_t)(i - kStackMax) * ostride] = v;
+    }
+    __device__ __forceinline__ int get(int i) const {
+        return i < kStackMax ? lds[i * kBlock] : ovf[(size_t)(i - kStackMax) * ostride];
+    }
+};
+// this thread's stack: stk_all = the block's LDS array, tid = the thread's index in the launch grid
+__device__ __forceinline__ Stk make_stk(const DScene& S, int* stk_all) {
+    Stk s;
+    s.lds = stk_all + threadIdx.x;
+    s.ostride = gridDim.x * kBlock;
+    s.ovf = S.stk_ovf ? S.stk_ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) : nullptr;
+    return s;
+}
 #ifdef RS_TRAV_STATS
 // all 64 lanes converged: per ray sums, per wave the max node count (the wave runs the union of its
 // lanes' loops) and the wave's live lanes
@@ -262,7 +285,7 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
 }
 #endif
 template <int SM>
-__device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, int* stk) {
+__device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
     if (S.root < 0) return -1;
     const RayC rc = ray_consts(r);
     const RayF rf = make_rayf(r.o, rc.inv);
@@ -327,17 +350,23 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
             int next;
             if (cnt == 0) {
                 next = -1;
-                if (sp > 0) { --sp; next = stk[sp * kBlock]; }
+                if (sp > 0) { --sp; next = stk.get(sp); }
             } else {
                 // sort descending by entry (farthest first, not-visited last): 5 compare-swaps
 #define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
                 RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
 #undef RS_CS
-                // the cnt - 1 farther children are pushed; the writes above them are dead (the
-                // host keeps 3 * levels <= kStackMax, so sp + 2 stays inside the column)
-                stk[sp * kBlock] = n0;
-                stk[(sp + 1) * kBlock] = n1;
-                stk[(sp + 2) * kBlock] = n2;
+                // the cnt - 1 farther children are pushed; inside the LDS part all three writes are
+                // issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
+                if (sp + 3 <= kStackMax) {
+                    stk.lds[sp * kBlock] = n0;
+                    stk.lds[(sp + 1) * kBlock] = n1;
+                    stk.lds[(sp + 2) * kBlock] = n2;
+                } else {
+                    if (cnt > 1) stk.put(sp, n0);
+                    if (cnt > 2) stk.put(sp + 1, n1);
+                    if (cnt > 3) stk.put(sp + 2, n2);
+                }
                 sp += cnt - 1;
                 next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
             }
@@ -377,7 +406,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
             if (h0 && h1) {
                 int nn = c0, ff = c1;
                 if (e1 < e0) { nn = c1; ff = c0; }
-                stk[sp * kBlock] = ff;
+                stk.put(sp, ff);
                 ++sp;
                 node = nn;
             } else if (h0) {
@@ -387,7 +416,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
             } else {
                 if (sp == 0) break;
                 --sp;
-                node = stk[sp * kBlock];
+                node = stk.get(sp);
             }
         }
     } else {
@@ -401,7 +430,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
                     if (c0 < 0) {
                         RS_LEAF(c0);
                     } else {
-                        stk[sp * kBlock] = node;  // come back for the right child
+                        stk.put(sp, node);  // come back for the right child
                         ++sp;
                         node = c0;
                         continue;
@@ -420,7 +449,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
             }
             if (sp == 0) break;
             --sp;
-            node = stk[sp * kBlock];
+            node = stk.get(sp);
             second = true;
         }
     }
@@ -446,7 +475,7 @@ __device__ __forceinline__ bool finish_hit(const DScene& S, int bp, const Ray& r
 }
 
 template <int SM>
-__device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, int* stk) {
+__device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, const Stk& stk) {
     double bend;
     const int bp = traverse<SM>(S, r, tmin, bend, stk);
     return finish_hit<SM>(S, bp, r, tmin, bend, h);
@@ -604,7 +633,7 @@ __device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray,
 
 // ray_color iterated: one world.hit per level, at most `depth` levels. Returns the radiance.
 template <int SM>
-__device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, int* stk, uint32_t& segs) {
+__device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, const Stk& stk, uint32_t& segs) {
     V3 T = v3(1.0, 1.0, 1.0);
     V3 L = v3(0.0, 0.0, 0.0);
     for (uint32_t d = depth; d > 0; --d) {
@@ -621,10 +650,11 @@ template <int SM>
 __global__ __launch_bounds__(kBlock) void k_path_mega(DScene S, DCamera C, PathParams P, double* __restrict__ rad,
                                                       unsigned long long* __restrict__ seg_counters) {
     __shared__ int stk_all[kStackMax * kBlock];
-    int* stk = stk_all + threadIdx.x;
-    const uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const Stk stk = make_stk(S, stk_all);
     uint32_t segs = 0;
-    if (item < P.n_items) {
+    // grid-stride (the host bounds the grid, which also bounds the stack overflow array)
+    for (uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x; item < P.n_items;
+         item += (uint64_t)gridDim.x * kBlock) {
         const uint32_t pl = (uint32_t)(item % P.n_pix_local);
         const uint32_t sl = (uint32_t)(item / P.n_pix_local);
         const uint32_t x = pl % P.width;
@@ -796,7 +826,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
 template <int SM>
 __global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) void k_wf_extend(DScene S, WfState W, uint32_t bounce) {
     __shared__ int stk_all[kStackMax * kBlock];
-    int* stk = stk_all + threadIdx.x;
+    const Stk stk = make_stk(S, stk_all);
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
@@ -861,7 +891,7 @@ __global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(DScene 
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
     __shared__ int stk_all[kStackMax * kBlock];
-    int* stk = stk_all + threadIdx.x;
+    const Stk stk = make_stk(S, stk_all);
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
     const uint32_t nf = GEN ? 0u : cnt[kCntFront];
     const uint32_t n = GEN ? n_gen : nf + cnt[kCntBack];
@@ -1148,7 +1178,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __
     for (int k = 0; k < 13; ++k) o[k] = 0.0;
     // range end handled by clamping best: world_hit starts from +inf, so emulate [tmin, tmax) by a
     // post-check only when tmax is infinite (the render path always passes +inf)
-    if (world_hit<kSmGeneric>(S, r, tmin, h, stk_all + threadIdx.x) && h.t1 < tmax) {
+    if (world_hit<kSmGeneric>(S, r, tmin, h, make_stk(S, stk_all)) && h.t1 < tmax) {
         o[0] = 1.0; o[1] = h.t1; o[2] = h.t2;
         o[3] = h.p.x; o[4] = h.p.y; o[5] = h.p.z; o[6] = h.n.x; o[7] = h.n.y; o[8] = h.n.z;
         if (S.uv) { o[9] = h.u; o[10] = h.v; }  // (u, v) exist only in scenes that read them
@@ -1176,7 +1206,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(DScene S, DCamera C, Pa
     Rng rng;
     camera_sample_xy(C, P, x, y, s0 + i, r, rng);
     uint32_t segs = 0;
-    const V3 L = trace_path<SM>(S, r, P.depth, rng, stk_all + threadIdx.x, segs);
+    const V3 L = trace_path<SM>(S, r, P.depth, rng, make_stk(S, stk_all), segs);
     out[4 * (size_t)i] = L.x; out[4 * (size_t)i + 1] = L.y; out[4 * (size_t)i + 2] = L.z;
     out[4 * (size_t)i + 3] = (double)segs;
 }
@@ -1190,8 +1220,8 @@ hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathPara
 }
 
 hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, int sm, double* rad,
-                            unsigned long long* seg_counters, hipStream_t st) {
-    const uint64_t blocks = (p.n_items + kBlock - 1) / kBlock;
+                            unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>((p.n_items + kBlock - 1) / kBlock, max_blocks);
     if (blocks == 0) return hipSuccess;
     RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_path_mega<SMC>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s, c, p, rad,
                                           seg_counters));

@@ -160,6 +160,10 @@ struct DScene {
     const int32_t* tex_i32;
     const uint8_t* tex_u8;
     const int32_t* lights;   // prim indices
+    // Traversal-stack overflow: entries [kStackMax, stack_need) of a thread's stack live in HBM,
+    // column (blockIdx.x * kBlock + threadIdx.x) of a [stack_need - kStackMax][gridDim.x * kBlock]
+    // array that the host sizes per launch grid (null when the tree fits the LDS stack).
+    int32_t* stk_ovf;
     int32_t n_lights;
     int32_t root;            // root child code (node index, or ~prim if a single object, or INT32_MIN if empty)
     int32_t default_mat;     // world.rs:51 Lambertian(Color(1,1,1,1))
@@ -167,7 +171,7 @@ struct DScene {
     int32_t root4;           // root of nodes4 (>= 0) when the 4-wide tree is used, else -1
     int32_t uv;              // 1: hit records carry (u, v) (some texture reads them: Image)
     int32_t has_media;       // 1: the scene has ConstantMedium objects (rays carry the medium key)
-    int32_t pad5;
+    int32_t stack_need;      // exact worst-case traversal stack depth of the tree in use (host-computed)
     float bg_lo[4], bg_hi[4];
 };
 
