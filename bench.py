@@ -1,10 +1,11 @@
 """bench.py — BASELINE metric: Msamples/s (whole node) + ms/frame on the RTIOW-13.1 scene
 (examples/rtow_13_1.rs: balls_scene seed 7 + light sphere) at 800x500, 64 spp, depth 8.
 
-A step = one frame pass of that workload per GPU (inputs resident in HBM: the scene is committed
-before timing, the frame lands in a device buffer). --split passes (default, weak scaling): rank
-r renders progressive pass r and the passes are combined at frame end (RCCL all_gather);
---split rows (strong scaling): the frame's rows are interleaved over ranks and gathered.
+A step = one frame of that workload (inputs resident in HBM: the scene is committed before timing,
+the frame lands in a device buffer). --split rows (default, strong scaling): the frame's rows are
+interleaved over ranks like render_rows (painter.rs:248) and gathered to rank 0 at frame end (one
+RCCL gather), so N = 1 and N = 8 render the same frame; --split passes (weak scaling): rank r renders
+progressive pass r of the whole frame and rank 0 folds the passes (raysnail.rs:379-427).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
 torch.distributed.run with one rank per GPU. Rank 0 prints one JSON line.
@@ -27,6 +28,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpus():
+    """What raysnail's thread count sees on this host: num_cpus 1.13.0 get() (Cargo.lock:345-347) =
+    the CPUs in the process's affinity mask; Painter::draw uses get() + 1 threads (painter.rs:321-325).
+    Also the CPU model and the cgroup CPU quota (which caps the threads' combined throughput)."""
+    n = len(os.sched_getaffinity(0))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return n, model, quota
+
+
 def cpu_baseline(cam, world, spp, depth, seed, row_step, threads):
     """The oracle (C++ restatement of Painter::draw, f64, row-interleaved threads) on a bounded row
     subset of the same frame. kind = 'port'."""
@@ -39,22 +63,26 @@ def cpu_baseline(cam, world, spp, depth, seed, row_step, threads):
     t0 = time.perf_counter()
     _, stats = sc.render(cam.desc, st, threads=threads)
     dt = time.perf_counter() - t0
+    n, model, quota = host_cpus()
     return {"value": stats.samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"rows 0::{row_step} of the 800x500x64 frame ({stats.samples} samples, "
-                      f"{stats.segments} segments) in {dt:.1f} s, {threads} threads, oracle/oracle.cpp f64"}
+            "threads": threads, "nproc": n, "cpu_model": model, "cgroup_cpu_quota": quota,
+            "sample": f"rows 0::{row_step} of the frame ({stats.samples} samples, {stats.segments} segments) "
+                      f"in {dt:.1f} s, {threads} threads (num_cpus {n} + 1, painter.rs:321-325) on {model}"
+                      + (f" under a {quota}-CPU cgroup quota" if quota else "") + ", oracle/oracle.cpp f64"}
 
 
 def load_pmc(kernel_prefix):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary (tools/collect_pmc.py)."""
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (tools/collect_pmc.py) and the
+    profile round it was measured in (the field is only valid while the kernels are unchanged)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         d = json.load(open(path))
         k = d.get(kernel_prefix)
-        return None if k is None else float(k["hbm_bytes_per_launch"])
+        return (None if k is None else float(k["hbm_bytes_per_launch"])), d.get("_round")
     except Exception:
-        return None
+        return None, None
 
 
 def main():
@@ -67,11 +95,11 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--split", choices=["passes", "rows"], default="passes")
+    ap.add_argument("--split", choices=["passes", "rows"], default="rows")
     ap.add_argument("--mode", type=int, default=0, help="RS_MODE_* (0 auto)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-row-step", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = num_cpus + 1 like Painter::draw")
     args = ap.parse_args()
 
     import torch
@@ -147,9 +175,9 @@ def main():
         avg_launch_s = kern_ms / max(1, kern_launches) / 1e3
         bytes_per_launch = kern_bytes / max(1, kern_launches)
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        traffic = load_pmc(kname) if kname else None
+        traffic, traffic_round = load_pmc(kname) if kname else (None, None)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_profile": traffic_round,
                 "kernel": kname, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "alg_bytes_per_launch": int(bytes_per_launch), "launches_per_step": kern_launches // args.steps,
                 "kernel_share_of_step": round(kern_ms / args.steps / (dt / args.steps * 1e3), 4),
@@ -158,7 +186,7 @@ def main():
         if args.cpu_baseline and world == 1:
             log("timing CPU baseline (oracle restatement) ...")
             cpu = cpu_baseline(cam, scene_world, args.spp, args.depth, args.seed, args.cpu_row_step,
-                               args.cpu_threads)
+                               args.cpu_threads or host_cpus()[0] + 1)
         line = {
             "metric": "Msamples/s (whole node) + ms/frame, RTIOW-13.1 scene 800x500x64spp",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,

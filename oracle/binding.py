@@ -63,6 +63,11 @@ def load(path: str = LIB_PATH) -> C.CDLL:
                                 C.POINTER(C.c_double)]
     lib.orc_scatter.restype = C.c_int
     lib.orc_set_trace.argtypes = [C.c_int]
+    lib.orc_chacha_block.argtypes = [C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_uint32)]
+    lib.orc_rtow_balls.argtypes = [C.c_uint64, C.POINTER(C.c_double), C.c_int]
+    lib.orc_rtow_balls.restype = C.c_int
+    lib.orc_rtow_scene.argtypes = [C.c_void_p, C.c_uint64]
+    lib.orc_rtow_scene.restype = C.c_int
     _LIBS[path] = lib
     return lib
 
@@ -71,10 +76,14 @@ class OracleScene:
     """The same World replayed into the CPU restatement (or, with world=None, filled by
     `fill(api, handle)` through a sink table -- e.g. the C++ SDL front end)."""
 
-    def __init__(self, world: World = None, fill=None, lib_path: str = LIB_PATH):
+    def __init__(self, world: World = None, fill=None, lib_path: str = LIB_PATH, rtow_seed: int = None):
+        """rtow_seed: the RTIOW final scene (examples/rtow_13_1.rs) built by the oracle's own C++
+        generator (oracle/scene_gen.cpp), independent of raysnail_amd/scenes.py."""
         self.lib = load(lib_path)
         self.h = C.c_void_p(self.lib.orc_scene_create())
-        if world is not None:
+        if rtow_seed is not None:
+            _check(self.lib, self.lib.orc_rtow_scene(self.h, rtow_seed), "orc_")
+        elif world is not None:
             realize(world, self.lib, self.h, "orc_")
         else:
             from raysnail_amd.host_lib import sink_api_of
@@ -113,3 +122,12 @@ class OracleScene:
         _check(self.lib, self.lib.orc_world_hit(self.h, (C.c_double * 3)(*o), (C.c_double * 3)(*d), time, tmin, tmax,
                                                 out), "orc_")
         return list(out)
+
+
+def rtow_balls(seed: int = 7) -> np.ndarray:
+    """The oracle's own RTIOW ball list (scene_gen.cpp): rows cx cy cz r kind checker r g b param 0 0."""
+    lib = load()
+    n = lib.orc_rtow_balls(seed, None, 0)
+    out = np.zeros((n, 12))
+    lib.orc_rtow_balls(seed, out.ctypes.data_as(C.POINTER(C.c_double)), n)
+    return out

@@ -829,12 +829,18 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) v
     const Stk stk = make_stk(S, stk_all);
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        Ray r = load_ray(cur, i);
-        if (rich_of(SM) && S.has_media) r.key = load_rng(cur, i).medium_key();  // the segment's medium key
-        double bend = RS_INF;
-        const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
-        W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        if (i < n) {
+            Ray r = load_ray(cur, i);
+            if (rich_of(SM) && S.has_media) r.key = load_rng(cur, i).medium_key();  // the segment's medium key
+            double bend = RS_INF;
+            const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
+            W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+        }
+#ifdef RS_TRAV_STATS
+        trav_stats_flush(i < n);
+#endif
     }
 }
 

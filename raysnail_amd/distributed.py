@@ -6,11 +6,11 @@ i, i+T, ... and Painter::append de-interleaves them). The GPU path keeps both of
 natural shardings, each with a single exchange at frame end:
 
 * ``rows``   — one frame, rows interleaved over ranks exactly like render_rows (row r on rank
-               r % N); ranks pack their rows, all_gather them and de-interleave (= append,
-               painter.rs:220-236). Strong scaling; the assembled frame is bitwise equal to the
-               1-GPU frame because every sample has its own RNG stream.
+               r % N); ranks pack their rows, gather them to rank 0 and it de-interleaves them
+               (= append, painter.rs:220-236). Strong scaling; the assembled frame is bitwise
+               equal to the 1-GPU frame because every sample has its own RNG stream.
 * ``passes`` — the CLI's progressive passes (src/bin/raysnail.rs:379-427): rank r renders pass r
-               of the whole frame; the N pass frames are gathered and folded in pass order with
+               of the whole frame; the N pass frames are gathered to rank 0 and folded in pass order with
                combine_pixel (raysnail.rs:176-208). Weak scaling: per-GPU work is one full pass.
 
 The renderer is injected (``render(row_begin, row_end, row_step, pass_index) -> (H, W, 4)``), so
@@ -33,8 +33,10 @@ def rows_of(rank: int, world: int, height: int) -> int:
     return (height - rank + world - 1) // world if rank < height else 0
 
 
-def gather_rows(frame: torch.Tensor, rank: int, world: int) -> torch.Tensor:
-    """frame: (H, W, 4) with this rank's lattice rows rendered. Returns the full frame on every rank."""
+def gather_rows(frame: torch.Tensor, rank: int, world: int, dst: int = 0):
+    """frame: (H, W, 4) with this rank's lattice rows rendered. Each rank packs its rows and sends
+    them to rank `dst` (one RCCL gather at frame end), which de-interleaves them (Painter::append,
+    painter.rs:220-236). Returns the full frame on dst, None elsewhere."""
     H = frame.shape[0]
     if world == 1:
         return frame
@@ -42,8 +44,10 @@ def gather_rows(frame: torch.Tensor, rank: int, world: int) -> torch.Tensor:
     mine = frame[rank::world]
     packed = torch.zeros((per,) + tuple(frame.shape[1:]), dtype=frame.dtype, device=frame.device)
     packed[: mine.shape[0]] = mine
-    parts = [torch.empty_like(packed) for _ in range(world)]
-    dist.all_gather(parts, packed)
+    parts = [torch.empty_like(packed) for _ in range(world)] if rank == dst else None
+    dist.gather(packed, parts, dst=dst)
+    if rank != dst:
+        return None
     out = torch.empty_like(frame)
     for r in range(world):
         n = rows_of(r, world, H)
@@ -65,8 +69,8 @@ def gather_passes(frame: torch.Tensor, rank: int, world: int, dst: int = 0):
     if world == 1:
         parts = [frame]
     else:
-        parts = [torch.empty_like(frame) for _ in range(world)]
-        dist.all_gather(parts, frame)
+        parts = [torch.empty_like(frame) for _ in range(world)] if rank == dst else None
+        dist.gather(frame, parts, dst=dst)
     if rank != dst:
         return None
     acc = torch.zeros_like(frame)

@@ -146,6 +146,12 @@ Image Image::open(const std::string& path) {
     if (!w || !h || channels == 0) throw Error(RS_E_INVALID, "Image: bad PNG header");
     if (depth != 8 || interlace != 0)
         throw Error(RS_E_UNSUPPORTED, "Image: only 8-bit, non-interlaced PNGs are supported");
+    // bound the header before sizing buffers from it (a crafted IHDR must fail, not overflow):
+    // each side <= 2^24, decoded bytes (incl. one filter byte per row) <= 2^31, zlib sizes < 2^32
+    if (w > (1u << 24) || h > (1u << 24)) throw Error(RS_E_INVALID, "Image: PNG dimensions too large");
+    const uint64_t raw_bytes = ((uint64_t)w * (uint64_t)channels + 1) * (uint64_t)h;
+    if (raw_bytes > (1ull << 31)) throw Error(RS_E_INVALID, "Image: PNG image too large (> 2 GiB decoded)");
+    if (idat.size() > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "Image: PNG image data too large");
     const size_t stride = (size_t)w * channels;
     std::vector<uint8_t> raw((stride + 1) * h);
     z_stream zs;

@@ -100,6 +100,20 @@ def test_png_reader_rejects_bad_files(tmp_path):
         host_lib.png_load(str(tmp_path / "missing.png"))
 
 
+@pytest.mark.parametrize("w,h", [(2 ** 31, 2 ** 31), (1 << 25, 1), (1 << 24, 1 << 24), (0, 5)])
+def test_png_reader_rejects_oversized_headers(tmp_path, w, h):
+    """A crafted IHDR (sizes whose byte counts overflow 32/64-bit products) fails cleanly before any
+    buffer is sized from it; the reference's image crate fails safely on these too."""
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+    data = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 6, 0, 0, 0))
+    data += chunk(b"IDAT", zlib.compress(b"\x00" * 64)) + chunk(b"IEND", b"")
+    p = tmp_path / "big.png"
+    p.write_bytes(data)
+    with pytest.raises(host_lib.HostError):
+        host_lib.png_load(str(p))
+
+
 @pytest.mark.skipif(not os.path.exists(EARTH), reason="reference tree absent")
 def test_png_reader_on_reference_earth_map():
     """examples/earth-map.png (1920x960 RGB): the C++ reader against zlib + numpy unfiltering."""

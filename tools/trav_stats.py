@@ -9,8 +9,13 @@ import torch; torch.cuda.set_device(0)
 from raysnail_amd import scenes
 lib = _abi.load()
 out = (C.c_ulonglong * 8)()
-for name, build, spp, depth in (("rtow", lambda: scenes.rtow_13_1(800, 500)[:2], 64, 8),
-                                 ):
+CASES = {"rtow": (lambda: scenes.rtow_13_1(800, 500)[:2], 64, 8),
+         "mesh": (lambda: scenes.mesh_scene(960, 540), 16, 50),
+         "example": (lambda: scenes.example_sdl(800, 500), 16, 50),
+         "quadric": (lambda: scenes.quadric_sdl(512, 512), 16, 50)}
+names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["rtow"]
+for name in names:
+    build, spp, depth = CASES[name]
     cam, world = build()
     photo = cam.take_photo().samples(spp).depth(depth).seed(1)
     photo.shot(None, world)
