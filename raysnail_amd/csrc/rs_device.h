@@ -169,6 +169,46 @@ __device__ __forceinline__ bool rect_hit_raw(int ax0, int ax1, int ax2, double k
     return true;
 }
 
+// Box::hit's (t1, t2) alone (box.rs:125-149): the first two face hits in face order; one -> (t, MAX),
+// two -> (nearer, farther). What the traversal and the CSG decisions read (the record: box_hit).
+__device__ __forceinline__ bool box_t(const DBox& b, const Ray& r, double tmin, double tmax, double& t1o, double& t2o) {
+    double ta = 0.0, tb = 0.0;
+    int n = 0;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+        int ax0, ax1, ax2; double k, a0, a1, b0, b1;
+        if (f < 2)      { ax0 = 0; ax1 = 1; ax2 = 2; k = f == 0 ? b.mn[2] : b.mx[2]; a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[1]; b1 = b.mx[1]; }
+        else if (f < 4) { ax0 = 1; ax1 = 2; ax2 = 0; k = f == 2 ? b.mn[0] : b.mx[0]; a0 = b.mn[1]; a1 = b.mx[1]; b0 = b.mn[2]; b1 = b.mx[2]; }
+        else            { ax0 = 0; ax1 = 2; ax2 = 1; k = f == 4 ? b.mn[1] : b.mx[1]; a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[2]; b1 = b.mx[2]; }
+        if (n < 2) {
+            const double t = (k - comp(r.o, ax2)) / comp(r.d, ax2);
+            if (in_range(t, tmin, tmax)) {
+                const double a = fma(t, comp(r.d, ax0), comp(r.o, ax0));
+                const double bb = fma(t, comp(r.d, ax1), comp(r.o, ax1));
+                if (!(a < a0 || a > a1) && !(bb < b0 || bb > b1)) {
+                    if (n == 0) ta = t; else tb = t;
+                    ++n;
+                }
+            }
+        }
+    }
+    if (n == 0) return false;
+    if (n == 1) { t1o = ta; t2o = RS_FMAX; return true; }
+    if (ta < tb) { t1o = ta; t2o = tb; } else { t1o = tb; t2o = ta; }
+    return true;
+}
+
+__device__ __forceinline__ bool rect_t(const DRect& R, const Ray& r, double tmin, double tmax, double& t1) {
+    const double t = (R.k - comp(r.o, R.ax2)) / comp(r.d, R.ax2);
+    if (!in_range(t, tmin, tmax)) return false;
+    const double a = fma(t, comp(r.d, R.ax0), comp(r.o, R.ax0));
+    if (a < R.a0 || a > R.a1) return false;
+    const double b = fma(t, comp(r.d, R.ax1), comp(r.o, R.ax1));
+    if (b < R.b0 || b > R.b1) return false;
+    t1 = t;
+    return true;
+}
+
 // box.rs:125-149; faces in the order built by box.rs:55-105
 __device__ bool box_hit(const DBox& b, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h, int uv = 0) {
     Hit h0, h1;  // the first two face hits in face order (two named records: no scratch array)
@@ -210,6 +250,32 @@ __device__ V3 quadric_normal(const DQuadric& Q, V3 p) {
     if (len == 0.0) return v3(1.0, 0.0, 0.0);
     return vdiv(rr, len);
 }
+// Quadric::hit's (t1, t2) alone (quadric.rs:112-182; the record: quadric_hit)
+__device__ __forceinline__ bool quadric_t(const DQuadric& Q, const Ray& r, double tmin, double tmax, double& t1, double& t2) {
+    const double* q = Q.q;
+    const double qa = q[0], qb = q[1], qc = q[2], qd = q[3], qe = q[4], qf = q[5], qg = q[6], qh = q[7], qi = q[8], qj = q[9];
+    double xo = r.o.x, yo = r.o.y, zo = r.o.z, xd = r.d.x, yd = r.d.y, zd = r.d.z;
+    double a = xd * (qa * xd + qb * yd + qc * zd) + yd * (qe * yd + qf * zd) + zd * qh * zd;
+    double b = xd * (qa * xo + 0.5 * (qb * yo + qc * zo + qd)) + yd * (qe * yo + 0.5 * (qb * xo + qf * zo + qg)) +
+               zd * (qh * zo + 0.5 * (qc * xo + qf * yo + qi));
+    double c = xo * (qa * xo + qb * yo + qc * zo + qd) + yo * (qe * yo + qf * zo + qg) + zo * (qh * zo + qi) + qj;
+    if (a == 0.0) {
+        if (b == 0.0) return false;
+        t1 = -0.5 * c / b;
+        if (!in_range(t1, tmin, tmax)) return false;
+        t2 = RS_FMAX;
+        return true;
+    }
+    double d = b * b - a * c;
+    if (d <= 0.0) return false;
+    double dr = sqrt(d);
+    double r1 = (-b - dr) / a;
+    double r2 = (-b + dr) / a;
+    if (in_range(r1, tmin, tmax)) { t1 = r1; t2 = r2; return true; }
+    if (in_range(r2, tmin, tmax)) { t1 = r2; t2 = RS_FMAX; return true; }
+    return false;
+}
+
 // quadric.rs:112-182
 __device__ bool quadric_hit(const DQuadric& Q, int32_t mat, const Ray& r, double tmin, double tmax, Hit& h, int uv = 0) {
     const double* q = Q.q;
@@ -247,8 +313,12 @@ __device__ __forceinline__ bool quadric_contains(const DQuadric& Q, V3 p) {  // 
 }
 
 // triangle_mesh.rs:85-131
-// tri_hit's accept test alone (the traversal's leaf test; the winner's record is recomputed)
-__device__ __forceinline__ bool tri_t(const DTri& T, const Ray& r, double tmin, double tmax, double& t_out) {
+// tri_hit's accept test alone (the traversal's leaf test; the winner's record is recomputed).
+// TRI: DTri or the leaf-ordered LTri (same p0 / a..f fields). (Skipping the divisions for lanes whose
+// quotient sign / magnitude already rejects was measured slower: under divergence the wave still runs
+// the division for its other lanes, and the extra registers spilled the flat-scene extend.)
+template <typename TRI>
+__device__ __forceinline__ bool tri_t(const TRI& T, const Ray& r, double tmin, double tmax, double& t_out) {
     double g = r.d.x, hh = r.d.y, i = r.d.z;
     double j = T.p0[0] - r.o.x, k = T.p0[1] - r.o.y, l = T.p0[2] - r.o.z;
     double eihf = T.e * i - hh * T.f;
@@ -312,13 +382,107 @@ __device__ __forceinline__ V3 tf_inverse(const DScene& S, const DXform& X, int n
 // records with (u, v)), 0 elsewhere, so the common kernels carry none of that code.
 template <int L, int R> struct Obj;
 
+// What the traversal and the CSG decisions read of a hit() record: t1, t2 and the point (a TfFacade
+// record's point is mapped forward, so it is not always ray.at(t1)). hit_t decides exactly what hit()
+// decides and returns these fields bit for bit; hit() builds the full record of the one object that
+// won (CSG: the winning child's own hit()), so no Hit records are live during the decisions.
+struct HitT { double t1, t2; V3 p; };
+
 template <int R> struct Obj<-1, R> {
     static __device__ bool hit(const DScene&, int, const Ray&, double, double, Hit&) { return false; }
+    static __device__ bool hit_t(const DScene&, int, const Ray&, double, double, HitT&) { return false; }
     static __device__ bool contains(const DScene&, int, V3) { return false; }
     static __device__ V3 random(const DScene&, int, V3, Rng&) { return v3(1.0, 0.0, 0.0); }
 };
 
 template <int L, int R> struct Obj {
+    // inlined in the scene modes with at most two nesting levels (no call frames and no spills in
+    // their traversal loops); the generic mode's up-to-4-level copies stay calls (code size)
+    static __device__ __forceinline__ bool hit_t(const DScene& S, int pi, const Ray& r, double tmin, double tmax, HitT& h) {
+        if constexpr (L <= 2 && R == 0) return hit_t_body(S, pi, r, tmin, tmax, h);
+        else return hit_t_call(S, pi, r, tmin, tmax, h);
+    }
+    static __device__ __noinline__ bool hit_t_call(const DScene& S, int pi, const Ray& r, double tmin, double tmax, HitT& h) {
+        return hit_t_body(S, pi, r, tmin, tmax, h);
+    }
+    static __device__ __forceinline__ bool hit_t_body(const DScene& S, int pi, const Ray& r, double tmin, double tmax,
+                                                     HitT& h) {
+        const DPrim P = S.prims[pi];
+        switch (P.kind) {
+        case PK_SPHERE: {
+            double t, t2;
+            if (!sphere_t(S.spheres[P.idx], r, tmin, tmax, t, t2)) return false;
+            h.t1 = t; h.t2 = t2; h.p = ray_at(r, t);
+            return true;
+        }
+        case PK_RECT:
+            if (!rect_t(S.rects[P.idx], r, tmin, tmax, h.t1)) return false;
+            h.t2 = RS_FMAX; h.p = ray_at(r, h.t1);
+            return true;
+        case PK_BOX:
+            if (!box_t(S.boxes[P.idx], r, tmin, tmax, h.t1, h.t2)) return false;
+            h.p = ray_at(r, h.t1);
+            return true;
+        case PK_QUADRIC:
+            if (!quadric_t(S.quadrics[P.idx], r, tmin, tmax, h.t1, h.t2)) return false;
+            h.p = ray_at(r, h.t1);
+            return true;
+        case PK_TRIANGLE:
+            if (!tri_t(S.tris[P.idx], r, tmin, tmax, h.t1)) return false;
+            h.t2 = RS_FMAX; h.p = ray_at(r, h.t1);
+            return true;
+        case PK_AND: {  // csg/intersection.rs:58-100
+            const DCsg C = S.csgs[P.idx];
+            HitT h1, h2;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, h1)) return false;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, h2)) return false;
+            const bool first1 = h1.t1 < h2.t1;
+            const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
+            const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
+            if (Obj<L - 1, R>::contains(S, o1, p0)) h = first1 ? h1 : h2;
+            else if (Obj<L - 1, R>::contains(S, o0, p1)) h = first1 ? h2 : h1;
+            else return false;
+            return true;
+        }
+        case PK_SUB: {  // csg/difference.rs:57-106
+            const DCsg C = S.csgs[P.idx];
+            HitT hp, hm;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, hp)) return false;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, hm)) { h = hp; return true; }
+            if (hp.t1 < hm.t1) {
+                if (Obj<L - 1, R>::contains(S, C.b, hp.p)) return false;
+                h = hp;
+            } else if (hm.t2 < hp.t1) {
+                h = hp;
+            } else if (hm.t2 < hp.t2) {
+                h.p = ray_at(r, hm.t2); h.t1 = hm.t2; h.t2 = hp.t2;
+            } else {
+                return false;
+            }
+            return true;
+        }
+        case PK_XFORM: {  // tf_facade.rs:41-55
+            const DXform X = S.xforms[P.idx];
+            Ray rr;
+            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
+            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
+            rr.time = r.time;
+            if (R) rr.key = r.key;
+            if (!Obj<L - 1, R>::hit_t(S, X.child, rr, tmin, tmax, h)) return false;
+            h.p = tf_forward(S, X, P.aux, h.p, 1.0);
+            return true;
+        }
+        case PK_MEDIUM: {  // the record is cheap; reuse it (rich scene mode only)
+            if (!R) return false;
+            Hit f;
+            if (!hit(S, pi, r, tmin, tmax, f)) return false;
+            h.t1 = f.t1; h.t2 = f.t2; h.p = f.p;
+            return true;
+        }
+        }
+        return false;
+    }
+
     static __device__ bool hit(const DScene& S, int pi, const Ray& r, double tmin, double tmax, Hit& h) {
         const DPrim P = S.prims[pi];
         switch (P.kind) {
@@ -330,33 +494,34 @@ template <int L, int R> struct Obj {
         case PK_BOX: return box_hit(S.boxes[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         case PK_QUADRIC: return quadric_hit(S.quadrics[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         case PK_TRIANGLE: return tri_hit(S.tris[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
-        case PK_AND: {  // csg/intersection.rs:58-100
+        case PK_AND: {  // csg/intersection.rs:58-100: decided on (t1, t2, p), then the winner's record
             const DCsg C = S.csgs[P.idx];
-            Hit h1, h2;
-            bool ok1 = Obj<L - 1, R>::hit(S, C.a, r, tmin, tmax, h1);
-            bool ok2 = Obj<L - 1, R>::hit(S, C.b, r, tmin, tmax, h2);
-            if (!(ok1 && ok2)) return false;
+            HitT h1, h2;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, h1)) return false;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, h2)) return false;
             const bool first1 = h1.t1 < h2.t1;
             const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
             const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
-            if (Obj<L - 1, R>::contains(S, o1, p0)) { h = first1 ? h1 : h2; }
-            else if (Obj<L - 1, R>::contains(S, o0, p1)) { h = first1 ? h2 : h1; }
+            int win;
+            if (Obj<L - 1, R>::contains(S, o1, p0)) win = o0;
+            else if (Obj<L - 1, R>::contains(S, o0, p1)) win = o1;
             else return false;
+            Obj<L - 1, R>::hit(S, win, r, tmin, tmax, h);
             if (h.mat < 0) h.mat = P.mat;  // set_material_if_none (hit.rs:69-78)
             return true;
         }
         case PK_SUB: {  // csg/difference.rs:57-106
             const DCsg C = S.csgs[P.idx];
-            Hit hp, hm;
-            bool okp = Obj<L - 1, R>::hit(S, C.a, r, tmin, tmax, hp);
-            bool okm = Obj<L - 1, R>::hit(S, C.b, r, tmin, tmax, hm);
-            if (!okp) return false;
-            if (!okm) { h = hp; return true; }
-            if (hp.t1 < hm.t1) {
+            HitT hp, hm;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, hp)) return false;
+            bool plus;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, hm)) plus = true;
+            else if (hp.t1 < hm.t1) {
                 if (Obj<L - 1, R>::contains(S, C.b, hp.p)) return false;
-                h = hp;
-            } else if (hm.t2 < hp.t1) {
-                h = hp;
+                plus = true;
+            } else plus = hm.t2 < hp.t1;
+            if (plus) {
+                Obj<L - 1, R>::hit(S, C.a, r, tmin, tmax, h);
             } else if (hm.t2 < hp.t2) {
                 V3 p = ray_at(r, hm.t2);
                 V3 n = shape_normal(S, C.b, p);
@@ -404,7 +569,12 @@ template <int L, int R> struct Obj {
         return false;
     }
 
-    static __device__ bool contains(const DScene& S, int pi, V3 p) {
+    static __device__ __forceinline__ bool contains(const DScene& S, int pi, V3 p) {
+        if constexpr (L <= 2 && R == 0) return contains_body(S, pi, p);
+        else return contains_call(S, pi, p);
+    }
+    static __device__ __noinline__ bool contains_call(const DScene& S, int pi, V3 p) { return contains_body(S, pi, p); }
+    static __device__ __forceinline__ bool contains_body(const DScene& S, int pi, V3 p) {
         const DPrim P = S.prims[pi];
         switch (P.kind) {
         case PK_SPHERE: {  // sphere.rs:111-115

@@ -179,13 +179,25 @@ struct Replica {
     uint32_t** d_qptrs = nullptr;                 // device array of the per-class queues
     uint32_t* qptr[kWfsClasses] = {nullptr};
     int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond kStackMax)
+    DScene* d_ds = nullptr;                 // ds in device memory (what the kernels read)
+    DScene uploaded{};                      // the copy last written to d_ds
+
+    // the scene for a launch, with d_ds brought up to date first (it changes only when the
+    // stack-overflow array is reallocated)
+    SceneRef ref() {
+        if (std::memcmp(&uploaded, &ds, sizeof(DScene)) != 0) {
+            HIP_OK(hipMemcpy(d_ds, &ds, sizeof(DScene), hipMemcpyHostToDevice));
+            uploaded = ds;
+        }
+        return SceneRef{&ds, d_ds};
+    }
 
     ~Replica() {
         int prev = -1;
         const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
         for (void* p : dev) (void)hipFree(p);
         for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts,
-                        (void*)d_ovf})
+                        (void*)d_ovf, (void*)d_ds})
             if (p) (void)hipFree(p);
         if (stream) (void)hipStreamDestroy(stream);
         if (switched) (void)hipSetDevice(prev);
@@ -212,6 +224,7 @@ struct rs_scene {
     int tree_arity = 0;                     // 4: 4-wide tree, 2: binary tree, 0: empty world
     int stack_need = 0;                     // exact worst-case traversal stack depth of that tree
     size_t n_nodes = 0;
+    size_t n_leaf_entries = 0;
     double time0 = 0.0, time1 = 0.0;        // World::new time_limit (world.rs:40-53)
 
     uint32_t add(HObj o) {
@@ -355,8 +368,30 @@ DNode to_device(const HNode& h) {
 
 struct BuildItem { Box3 box; double c[3]; int32_t prim; };
 
+// Leaf entries in tree order (DScene::lprim): leaf code ~e names entry e (rs_layout.h).
+// With entries = false (scenes without leaf-ordered copies) a leaf code is ~prim.
+struct LeafSink {
+    bool entries = true;
+    std::vector<int32_t> prims;
+    template <typename It>
+    int32_t add(It first, It last) {
+        const size_t n = (size_t)(last - first);
+        if (n != 1) throw Error(RS_E_INVALID, "bad leaf size");
+        if (!entries) return ~*first;
+        if (prims.size() >= (size_t)INT32_MAX - 1) throw Error(RS_E_UNSUPPORTED, "too many objects for the BVH");
+        const int32_t e = (int32_t)prims.size();
+        prims.push_back(*first);
+        return ~e;
+    }
+};
+
 struct Builder {
     std::vector<HNode> nodes;
+    LeafSink* leaves = nullptr;
+    int max_leaf = 1;   // objects per leaf
+    int sah_depth = 48; // SAH splits above this depth, median splits below (bounds the depth)
+    static constexpr size_t kSweepMax = 1024;
+    static constexpr int kBins = 32;
     int max_depth = 0;
     static double area(const Box3& b) {
         double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
@@ -366,7 +401,12 @@ struct Builder {
     }
     // returns the child code of the subtree over items[b, e)
     int32_t build(std::vector<BuildItem>& it, size_t b, size_t e, int depth, Box3& out_box) {
-        if (e - b == 1) { out_box = it[b].box; return ~it[b].prim; }
+        if (e - b <= (size_t)max_leaf) {
+            out_box = it[b].box;
+            std::vector<int32_t> ps;
+            for (size_t i = b; i < e; ++i) { out_box = box_union(out_box, it[i].box); ps.push_back(it[i].prim); }
+            return leaves->add(ps.begin(), ps.end());
+        }
         max_depth = std::max(max_depth, depth + 1);
         Box3 cb = box_empty();
         for (size_t i = b; i < e; ++i)
@@ -376,20 +416,52 @@ struct Builder {
         double ext = -1;
         for (int k = 0; k < 3; ++k) if (cb.hi[k] - cb.lo[k] > ext) { ext = cb.hi[k] - cb.lo[k]; axis = k; }
         bool done = false;
-        if (depth < 12 && e - b > 2 && ext > 0) {  // SAH near the root, median below: depth <= 12 + log2(n)
-            // SAH over a full sweep of the centroid-sorted range on each axis
+        if (depth < sah_depth && e - b > 2 && ext > 0) {  // SAH above sah_depth, median below: depth <= sah_depth + log2(n)
             double best_cost = INFINITY; int best_axis = -1; size_t best_split = 0;
-            std::vector<double> right_area(e - b);
-            for (int k = 0; k < 3; ++k) {
-                if (!(cb.hi[k] - cb.lo[k] > 0)) continue;
-                std::stable_sort(it.begin() + b, it.begin() + e, [k](const BuildItem& x, const BuildItem& y) { return x.c[k] < y.c[k]; });
-                Box3 acc = box_empty();
-                for (size_t i = e; i-- > b + 1;) { acc = box_union(acc, it[i].box); right_area[i - b] = area(acc); }
-                acc = box_empty();
-                for (size_t i = b; i + 1 < e; ++i) {
-                    acc = box_union(acc, it[i].box);
-                    double cost = area(acc) * (double)(i + 1 - b) + right_area[i + 1 - b] * (double)(e - i - 1);
-                    if (cost < best_cost) { best_cost = cost; best_axis = k; best_split = i + 1; }
+            if (e - b <= kSweepMax) {
+                // small ranges: SAH over a full sweep of the centroid-sorted range on each axis
+                std::vector<double> right_area(e - b);
+                for (int k = 0; k < 3; ++k) {
+                    if (!(cb.hi[k] - cb.lo[k] > 0)) continue;
+                    std::stable_sort(it.begin() + b, it.begin() + e, [k](const BuildItem& x, const BuildItem& y) { return x.c[k] < y.c[k]; });
+                    Box3 acc = box_empty();
+                    for (size_t i = e; i-- > b + 1;) { acc = box_union(acc, it[i].box); right_area[i - b] = area(acc); }
+                    acc = box_empty();
+                    for (size_t i = b; i + 1 < e; ++i) {
+                        acc = box_union(acc, it[i].box);
+                        double cost = area(acc) * (double)(i + 1 - b) + right_area[i + 1 - b] * (double)(e - i - 1);
+                        if (cost < best_cost) { best_cost = cost; best_axis = k; best_split = i + 1; }
+                    }
+                }
+            } else {
+                // large ranges: binned SAH (kBins centroid bins per axis), then the range is ordered on
+                // the chosen axis so the left side is the first best_split - b items
+                for (int k = 0; k < 3; ++k) {
+                    const double lo = cb.lo[k], span = cb.hi[k] - cb.lo[k];
+                    if (!(span > 0) || !std::isfinite(span)) continue;
+                    const double scale = (double)kBins / span;
+                    Box3 bbox[kBins];
+                    size_t bcnt[kBins] = {0};
+                    for (int q = 0; q < kBins; ++q) bbox[q] = box_empty();
+                    for (size_t i = b; i < e; ++i) {
+                        const int q = std::min(kBins - 1, std::max(0, (int)((it[i].c[k] - lo) * scale)));
+                        bbox[q] = box_union(bbox[q], it[i].box);
+                        ++bcnt[q];
+                    }
+                    double rarea[kBins];
+                    size_t rcnt[kBins];
+                    Box3 acc = box_empty();
+                    size_t n = 0;
+                    for (int q = kBins - 1; q >= 1; --q) { acc = box_union(acc, bbox[q]); n += bcnt[q]; rarea[q] = area(acc); rcnt[q] = n; }
+                    acc = box_empty();
+                    n = 0;
+                    for (int q = 0; q + 1 < kBins; ++q) {
+                        acc = box_union(acc, bbox[q]);
+                        n += bcnt[q];
+                        if (n == 0 || rcnt[q + 1] == 0) continue;
+                        const double cost = area(acc) * (double)n + rarea[q + 1] * (double)rcnt[q + 1];
+                        if (cost < best_cost) { best_cost = cost; best_axis = k; best_split = b + n; }
+                    }
                 }
             }
             if (best_axis >= 0) {
@@ -421,9 +493,9 @@ struct Builder {
 // axis and one object per leaf: the tree the CPU oracle builds, so reference-order traversal
 // visits objects in the same sequence as the oracle's recursion.
 struct RefItem { Box3 box; double key_lo[3]; int32_t prim; };
-int32_t build_ref(std::vector<HNode>& nodes, std::vector<RefItem>& it, size_t b, size_t e, int depth, int& max_depth,
-                  Box3& out) {
-    if (e - b == 1) { out = it[b].box; return ~it[b].prim; }
+int32_t build_ref(std::vector<HNode>& nodes, LeafSink& leaves, std::vector<RefItem>& it, size_t b, size_t e, int depth,
+                  int& max_depth, Box3& out) {
+    if (e - b == 1) { out = it[b].box; return leaves.add(&it[b].prim, &it[b].prim + 1); }
     max_depth = std::max(max_depth, depth + 1);
     Box3 u = it[b].box;
     for (size_t i = b + 1; i < e; ++i) u = box_union(u, it[i].box);
@@ -437,8 +509,8 @@ int32_t build_ref(std::vector<HNode>& nodes, std::vector<RefItem>& it, size_t b,
     const int32_t idx = (int32_t)nodes.size();
     nodes.emplace_back();
     Box3 lb, rb;
-    const int32_t l = build_ref(nodes, it, b, mid, depth + 1, max_depth, lb);
-    const int32_t r = build_ref(nodes, it, mid, e, depth + 1, max_depth, rb);
+    const int32_t l = build_ref(nodes, leaves, it, b, mid, depth + 1, max_depth, lb);
+    const int32_t r = build_ref(nodes, leaves, it, mid, e, depth + 1, max_depth, rb);
     HNode& n = nodes[idx];
     std::memset(&n, 0, sizeof(n));
     for (int k = 0; k < 3; ++k) { n.lo[0][k] = lb.lo[k]; n.hi[0][k] = lb.hi[k]; n.lo[1][k] = rb.lo[k]; n.hi[1][k] = rb.hi[k]; }
@@ -553,6 +625,8 @@ void upload_replica(rs_scene* s, int device) {
         std::memcpy((char*)&R->ds + b.field_off, &p, sizeof(void*));
     }
     HIP_OK(hipMalloc((void**)&R->d_cnt, 512 * sizeof(unsigned long long)));
+    HIP_OK(hipMalloc((void**)&R->d_ds, sizeof(DScene)));
+    std::memset(&R->uploaded, 0xff, sizeof(DScene));  // forces the first upload
     HIP_OK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
@@ -708,6 +782,13 @@ void build(rs_scene* s) {
     for (uint32_t h : s->world) all_monotone = all_monotone && s->monotone(h);
     s->ref_order = !all_monotone;
     Builder B;
+    LeafSink leaves;
+    leaves.entries = s->scene_mode == kSmSpheres || s->scene_mode == kSmFlat;
+    B.leaves = &leaves;
+    // one object per leaf (measured on the C5 mesh: 2, 4 and 8 objects per leaf were 15 %, 45 % and
+    // 100 % slower -- a wave serialises its lanes' longer leaf loops)
+    B.max_leaf = 1;
+    if (const char* ev = std::getenv("RS_SAH_DEPTH")) B.sah_depth = std::max(0, std::atoi(ev));
     int32_t root = -1;
     if (!items.empty()) {
         Box3 rb;
@@ -722,7 +803,7 @@ void build(rs_scene* s) {
                 x.prim = (int32_t)h;
                 ri.push_back(x);
             }
-            code = build_ref(B.nodes, ri, 0, ri.size(), 0, B.max_depth, rb);
+            code = build_ref(B.nodes, leaves, ri, 0, ri.size(), 0, B.max_depth, rb);
         } else {
             code = B.build(items, 0, items.size(), 0, rb);
         }
@@ -794,12 +875,26 @@ void build(rs_scene* s) {
     d.stk_ovf = nullptr;  // sized per launch grid (ensure_stack_overflow)
     stage(s, d.prims, prims);
     stage(s, d.spheres, spheres);
-    if (s->spheres_only) {  // prim-indexed copy: the traversal's leaf test reads it without the DPrim hop
-        std::vector<DSphere> psph(s->objs.size());
-        std::memset(psph.data(), 0, psph.size() * sizeof(DSphere));
-        for (size_t h = 0; h < s->objs.size(); ++h)
-            if (s->objs[h].kind == PK_SPHERE) psph[h] = spheres[prims[h].idx];
-        stage(s, d.psph, psph);
+    // leaf entries in tree order + what each mode's leaf test reads, contiguous per leaf
+    stage(s, d.lprim, leaves.prims);
+    s->n_leaf_entries = leaves.prims.size();
+    if (s->scene_mode == kSmSpheres) {
+        std::vector<DSphere> lsph(leaves.prims.size());
+        for (size_t e = 0; e < lsph.size(); ++e) lsph[e] = spheres[prims[leaves.prims[e]].idx];
+        stage(s, d.lsph, lsph);
+    }
+    if (s->scene_mode == kSmFlat) {
+        std::vector<LTri> ltri(leaves.prims.size());
+        std::memset(ltri.data(), 0, ltri.size() * sizeof(LTri));
+        for (size_t e = 0; e < ltri.size(); ++e) {
+            const DPrim& P = prims[leaves.prims[e]];
+            ltri[e].kind = (double)P.kind;
+            if (P.kind != PK_TRIANGLE) continue;
+            const DTri& T = tris[P.idx];
+            for (int k = 0; k < 3; ++k) ltri[e].p0[k] = T.p0[k];
+            ltri[e].a = T.a; ltri[e].b = T.b; ltri[e].c = T.c; ltri[e].d = T.d; ltri[e].e = T.e; ltri[e].f = T.f;
+        }
+        stage(s, d.ltri, ltri);
     }
     stage(s, d.rects, rects);
     stage(s, d.boxes, boxes);
@@ -1098,7 +1193,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     P.kev.assign(2 * n_kernel_ev, nullptr);
     for (auto& e : P.ev) HIP_OK(hipEventCreate(&e));
     for (auto& e : P.kev) HIP_OK(hipEventCreate(&e));
-    const DScene& ds = R.ds;
+    const SceneRef ds = R.ref();
     HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
     if (wavefront && N > 0)
         HIP_OK(hipMemsetAsync(R.d_counts, 0, (size_t)n_chunks_total * (st->depth + 1) * cstride * sizeof(uint32_t), stream));
@@ -1703,7 +1798,7 @@ int rs_probe_world_hit(rs_scene* s, const double* rays, uint32_t n, double tmin,
         HIP_OK(hipMalloc((void**)&dout, (size_t)n * 13 * sizeof(double) + 8));
         HIP_OK(hipMemcpy(dr, rays, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice));
         ensure_stack_overflow(s, R, ((uint64_t)n + kBlock - 1) / kBlock * kBlock);
-        HIP_OK(launch_probe_hit(R.ds, dr, n, tmin, tmax, dout, nullptr));
+        HIP_OK(launch_probe_hit(R.ref(), dr, n, tmin, tmax, dout, nullptr));
         HIP_OK(hipMemcpy(out, dout, (size_t)n * 13 * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(dr);
         (void)hipFree(dout);
@@ -1729,7 +1824,7 @@ int rs_probe_samples(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
         double* dout = nullptr;
         HIP_OK(hipMalloc((void**)&dout, (size_t)n * 4 * sizeof(double) + 8));
         ensure_stack_overflow(s, R, ((uint64_t)n + kBlock - 1) / kBlock * kBlock);
-        HIP_OK(launch_probe_sample(R.ds, make_camera(*cam), pp, s->scene_mode, x, y, s0, n, dout, nullptr));
+        HIP_OK(launch_probe_sample(R.ref(), make_camera(*cam), pp, s->scene_mode, x, y, s0, n, dout, nullptr));
         HIP_OK(hipMemcpy(out, dout, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(dout);
     });

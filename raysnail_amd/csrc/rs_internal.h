@@ -24,6 +24,14 @@ constexpr int nest_of(int sm) { return sm == kSmNest0 ? 0 : sm == kSmNest2 ? 2 :
 // (commit puts every scene that uses them there; the other modes compile none of that code)
 constexpr int rich_of(int sm) { return sm == kSmGeneric ? 1 : 0; }
 
+// A committed scene for a launch: the host copy (launch decisions) and the same struct in device
+// memory, which the kernels read through a pointer (a by-value kernel argument that device functions
+// take by reference is copied to scratch).
+struct SceneRef {
+    const DScene* host;
+    const DScene* dev;
+};
+
 struct PathParams {
     uint64_t n_items;
     uint32_t n_pix_local;   // pixels on the row lattice
@@ -67,14 +75,14 @@ struct FinalParams {
 
 // Megakernel: one thread per (pixel, sample) path (grid-stride over at most max_blocks blocks);
 // radiance -> rad[c * n_items + item].
-hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
+hipError_t launch_probe_sample(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
                                uint32_t s0, uint32_t n, double* out, hipStream_t st);
-hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, int sm, double* rad,
+hipError_t launch_path_mega(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, double* rad,
                             unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st);
 hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
                          hipStream_t st);
-hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);
-hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
+hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);
+hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st);
 // material-sorted variant (every scene mode but the generic / rich one): counts stride per bounce = kWfsStride
 constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric, other
@@ -82,12 +90,12 @@ constexpr uint32_t kWfsStride = 8;
 // counts[6] / counts[7] of a bounce: paths written from the front / the back of the set (light-
 // sample rays / the rest), so the next extend's waves hold rays of one kind (k_wfs_shade)
 constexpr int kCntFront = 6, kCntBack = 7;
-hipError_t launch_wfs_gen_extend(const DScene& s, const DCamera& c, const PathParams& p, const WfState& w,
+hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
                                 uint32_t blocks, int sm, hipStream_t st);
-hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
+hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st);
-hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
                            hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
@@ -95,7 +103,7 @@ hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per
 hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st);
 hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, unsigned int* minmax_bits,
                         unsigned long long* count, hipStream_t st);
-hipError_t launch_probe_hit(const DScene& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
+hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
                             hipStream_t st);
 // acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic).
 hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch, int first_batch,

@@ -8,6 +8,8 @@
 // Build with -ffp-contract=off (see Makefile): the f64 arithmetic mirrors the reference's
 // operation order, so the only differences from the CPU oracle are ocml vs glibc ulps in
 // sin/cos/pow (documented tolerance in DESIGN.md).
+#include <cstdlib>
+
 #include "rs_device.h"
 #include "rs_internal.h"
 
@@ -173,8 +175,8 @@ __device__ __forceinline__ RayC ray_consts(const Ray& r) {
     return c;
 }
 
-// Sphere leaf: discriminant first, then the exact own box for spheres that hit.
-__device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int p, const Ray& r, const RayC& rc,
+// Sphere leaf (leaf entry e): discriminant first, then the exact own box for spheres that hit.
+__device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int e, const Ray& r, const RayC& rc,
                                                  double tmin, double& best, double& bend, int& bp) {
     double t;
     if (!sphere_t_trav(sp, r, rc.a, tmin, best, t)) return;
@@ -183,17 +185,21 @@ __device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere&
         lo[0] = sp.c[0] - sp.r; lo[1] = sp.c[1] - sp.r; lo[2] = sp.c[2] - sp.r;
         hi[0] = sp.c[0] + sp.r; hi[1] = sp.c[1] + sp.r; hi[2] = sp.c[2] + sp.r;
     } else {
-        const DBox64& B = S.pbox[p];
+        const DBox64& B = S.pbox[S.lprim ? S.lprim[e] : e];
         lo[0] = B.lo[0]; lo[1] = B.lo[1]; lo[2] = B.lo[2]; hi[0] = B.hi[0]; hi[1] = B.hi[1]; hi[2] = B.hi[2];
     }
     if (!slab64(lo, hi, r.o, rc.inv, tmin, best)) return;
-    bend = best; best = t; bp = p;
+    bend = best; best = t; bp = e;
 }
 
 // Nested-object entry points: Obj<L> instantiated only as deep as the scene mode needs.
 template <int SM>
 __device__ __forceinline__ bool obj_hit(const DScene& S, int p, const Ray& r, double tmin, double tmax, Hit& h) {
     return Obj<nest_of(SM), rich_of(SM)>::hit(S, p, r, tmin, tmax, h);
+}
+template <int SM>
+__device__ __forceinline__ bool obj_hit_t(const DScene& S, int p, const Ray& r, double tmin, double tmax, HitT& h) {
+    return Obj<nest_of(SM), rich_of(SM)>::hit_t(S, p, r, tmin, tmax, h);
 }
 template <int SM>
 __device__ __forceinline__ V3 obj_random(const DScene& S, int p, V3 origin, Rng& rng) {
@@ -212,31 +218,58 @@ __device__ __forceinline__ bool flat_hit(const DScene& S, const DPrim& P, const 
     return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, tmax, h, uv);
 }
 
-// Leaf: the object is accepted iff its exact own bbox passes (aabb.rs:20-38, BVH leaf box) AND it
-// hits within [tmin, best). Both are pure, so the cheap test runs first: for spheres the
-// discriminant, and the exact box only for spheres that hit.
+// Leaf entry e: its object is accepted iff its exact own bbox passes (aabb.rs:20-38, BVH leaf box)
+// AND it hits within [tmin, best). Both are pure, so the cheap test runs first: for spheres the
+// discriminant, for triangles the barycentric test, and the exact box only for those that hit.
+// On acceptance bp := e (traverse maps the winning entry to its prim handle at the end).
 template <int SM>
-__device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, const RayC& rc, double tmin, double& best,
+__device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, const RayC& rc, double tmin, double& best,
                                           double& bend, int& bp) {
-    if (SM == kSmSpheres) {  // prim-indexed sphere copy: one dependent load fewer than prims[p] -> spheres[idx]
-        test_sphere_leaf(S, S.psph[p], p, r, rc, tmin, best, bend, bp);
+    if (SM == kSmSpheres) {  // leaf-ordered sphere copy: no DPrim hop, a leaf's spheres contiguous
+        test_sphere_leaf(S, S.lsph[e], e, r, rc, tmin, best, bend, bp);
         return;
     }
+    if (SM == kSmFlat) {  // leaf-ordered triangle copy; its `kind` field says whether entry e is one
+        const LTri& T = S.ltri[e];
+        if (T.kind == (double)PK_TRIANGLE) {
+#if defined(RS_EXP_NOLEAF)  // dev experiment (wrong frames): the cost of the triangle leaf tests
+            return;
+#elif defined(RS_EXP_NOLEAFMATH)  // dev experiment: loads only
+            if (T.p0[0] == 12345.0) bp = e;
+            return;
+#endif
+            double t;
+            if (!tri_t(T, r, tmin, best, t)) return;
+            // the ray constants are recomputed here (accepted triangles only) instead of being kept
+            // live through the traversal: flat-scene extend runs at 5 waves on a 96-VGPR budget
+            const RayC lc = ray_consts(r);
+            const DBox64& B = S.pbox[S.lprim[e]];
+            if (!slab64(B.lo, B.hi, r.o, lc.inv, tmin, best)) return;
+            bend = best; best = t; bp = e;
+            return;
+        }
+        const int p = S.lprim[e];
+        const DPrim P = S.prims[p];
+        const RayC lc = ray_consts(r);
+        if (P.kind == PK_SPHERE) {
+            test_sphere_leaf(S, S.spheres[P.idx], e, r, lc, tmin, best, bend, bp);
+        } else {
+            const DBox64& B = S.pbox[p];
+            if (!slab64(B.lo, B.hi, r.o, lc.inv, tmin, best)) return;
+            Hit tmp;
+            if (flat_hit(S, P, r, tmin, best, tmp)) { bend = best; best = tmp.t1; bp = e; }
+        }
+        return;
+    }
+    const int p = S.lprim ? S.lprim[e] : e;  // nest / generic scenes' leaves name prims directly
     const DPrim P = S.prims[p];
     if (P.kind == PK_SPHERE) {
-        test_sphere_leaf(S, S.spheres[P.idx], p, r, rc, tmin, best, bend, bp);
-    } else if (SM == kSmFlat && P.kind == PK_TRIANGLE) {  // triangle first (most leaves fail its beta test)
-        double t;
-        if (!tri_t(S.tris[P.idx], r, tmin, best, t)) return;
-        const DBox64& B = S.pbox[p];
-        if (!slab64(B.lo, B.hi, r.o, rc.inv, tmin, best)) return;
-        bend = best; best = t; bp = p;
+        test_sphere_leaf(S, S.spheres[P.idx], e, r, rc, tmin, best, bend, bp);
     } else {
         const DBox64& B = S.pbox[p];
         if (!slab64(B.lo, B.hi, r.o, rc.inv, tmin, best)) return;
-        Hit tmp;
-        const bool ok = SM == kSmFlat ? flat_hit(S, P, r, tmin, best, tmp) : obj_hit<SM>(S, p, r, tmin, best, tmp);
-        if (ok) { bend = best; best = tmp.t1; bp = p; }
+        HitT tmp;  // t1 decides; the winner's record is built once, after the traversal (finish_hit)
+        if (obj_hit_t<SM>(S, p, r, tmin, best, tmp)) { bend = best; best = tmp.t1; bp = e; }
     }
 }
 
@@ -252,24 +285,25 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int p, const Ray& r, 
 // (stride kBlock), deeper ones in its column of the HBM overflow array (stride = grid threads).
 // The host sizes the overflow from the tree's exact worst-case depth, so any tree depth works;
 // scenes whose trees fit the LDS part never touch HBM (the bound test is one compare per push/pop).
+// The overflow address is formed only on the (rare) deep path, from the kernel-uniform base and the
+// thread's grid index, so the common path keeps no extra registers live.
 struct Stk {
-    int* lds;
-    int* ovf;
-    uint32_t ostride;
+    int* lds;          // this thread's column of the block's LDS stack
+    int* ovf_base;     // DScene::stk_ovf (uniform)
+    __device__ __forceinline__ int* ovf(int i) const {
+        return ovf_base + ((size_t)(i - kStackMax) * gridDim.x * kBlock + (size_t)blockIdx.x * kBlock + threadIdx.x);
+    }
     __device__ __forceinline__ void put(int i, int v) const {
         if (i < kStackMax) lds[i * kBlock] = v;
-        else ovf[(size_t)(i - kStackMax) * ostride] = v;
+        else *ovf(i) = v;
     }
-    __device__ __forceinline__ int get(int i) const {
-        return i < kStackMax ? lds[i * kBlock] : ovf[(size_t)(i - kStackMax) * ostride];
-    }
+    __device__ __forceinline__ int get(int i) const { return i < kStackMax ? lds[i * kBlock] : *ovf(i); }
 };
-// this thread's stack: stk_all = the block's LDS array, tid = the thread's index in the launch grid
+// this thread's stack (stk_all = the block's LDS array)
 __device__ __forceinline__ Stk make_stk(const DScene& S, int* stk_all) {
     Stk s;
     s.lds = stk_all + threadIdx.x;
-    s.ostride = gridDim.x * kBlock;
-    s.ovf = S.stk_ovf ? S.stk_ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) : nullptr;
+    s.ovf_base = S.stk_ovf;
     return s;
 }
 #ifdef RS_TRAV_STATS
@@ -284,8 +318,123 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
     if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); }
 }
 #endif
+// One node of the 4-wide near-first traversal: test the four child boxes of one 128-byte node,
+// push the farther inner children, test the node's leaves; returns the next node (-1: done).
+// Shared by traverse() and the persistent-lane flat-scene extend (k_wf_extend_pl).
+#ifdef RS_TRAV_STATS
+#define RS_ST_PARAMS , int& st_leaves
+#define RS_ST_PASS , st_leaves
+#else
+#define RS_ST_PARAMS
+#define RS_ST_PASS
+#endif
 template <int SM>
-__device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
+__device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const RayC& rc, const RayF4& rq, double tmin,
+                                 float tmin32, int node, int& sp, const Stk& stk, double& best, double& bend,
+                                 int& bp, float& best32 RS_ST_PARAMS) {
+#ifdef RS_TRAV_STATS
+#define RS_ST_LEAF4() ++st_leaves
+#else
+#define RS_ST_LEAF4()
+#endif
+#define RS_LEAF4(code)                                                         \
+    do {                                                                       \
+        RS_ST_LEAF4();                                                         \
+        const int bp_prev = bp;                                                \
+        test_leaf<SM>(S, ~(code), r, rc, tmin, best, bend, bp);                \
+        if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
+    } while (0)
+    float4 NX, FX, NY, FY, NZ, FZ;
+    int4 NC;
+    {
+        const char* nb = (const char*)(S.nodes4 + node);
+        NX = *(const float4*)(nb + rq.noff[0]); FX = *(const float4*)(nb + far_off(rq.noff[0], 0));
+        NY = *(const float4*)(nb + rq.noff[1]); FY = *(const float4*)(nb + far_off(rq.noff[1], 1));
+        NZ = *(const float4*)(nb + rq.noff[2]); FZ = *(const float4*)(nb + far_off(rq.noff[2], 2));
+        NC = *(const int4*)(nb + 96);
+    }
+    // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
+    // and tested after the four box tests, when the node's registers are dead. Branch-free:
+    // all four boxes are tested (the node's loads issue together) and the slot results are
+    // selects; an empty slot (INT32_MIN) is neither a leaf nor an inner child.
+    int n0, n1, n2, n3, l0, l1, l2, l3;
+    float e0, e1, e2, e3;
+#define RS_SLOT(K, NK, EK, LK)                                                                \
+    {                                                                                 \
+        float e;                                                                      \
+        const int c = NC.K;                                                           \
+        const bool hk = slab4(NX.K, NY.K, NZ.K, FX.K, FY.K, FZ.K, rq, tmin32, best32, e) & (c != INT32_MIN); \
+        LK = (hk & (c < 0)) ? c : INT32_MIN;                                          \
+        NK = c;                                                                       \
+        EK = (hk & (c >= 0)) ? e : -__builtin_huge_valf();                            \
+    }
+    RS_SLOT(x, n0, e0, l0) RS_SLOT(y, n1, e1, l1) RS_SLOT(z, n2, e2, l2) RS_SLOT(w, n3, e3, l3)
+#undef RS_SLOT
+    const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
+                    (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
+    int next;
+    if (cnt == 0) {
+        next = -1;
+        if (sp > 0) { --sp; next = stk.get(sp); }
+    } else {
+        // sort descending by entry (farthest first, not-visited last): 5 compare-swaps
+#define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
+        RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
+#undef RS_CS
+        // the cnt - 1 farther children are pushed; inside the LDS part all three writes are
+        // issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
+        if (sp + 3 <= kStackMax) {
+            stk.lds[sp * kBlock] = n0;
+            stk.lds[(sp + 1) * kBlock] = n1;
+            stk.lds[(sp + 2) * kBlock] = n2;
+        } else {
+            if (cnt > 1) stk.put(sp, n0);
+            if (cnt > 2) stk.put(sp + 1, n1);
+            if (cnt > 3) stk.put(sp + 2, n2);
+        }
+        sp += cnt - 1;
+        next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
+    }
+    // leaves of this node (their hits only shrink the range the next node is tested with),
+    // in slot order through ONE copy of the leaf test: every lane tests its k-th leaf in
+    // the same pass, so a wave runs max-over-lanes leaf tests per node, not one pass per
+    // slot that any lane uses
+#ifdef RS_LEAF_PER_SLOT
+    if (l0 != INT32_MIN) RS_LEAF4(l0);
+    if (l1 != INT32_MIN) RS_LEAF4(l1);
+    if (l2 != INT32_MIN) RS_LEAF4(l2);
+    if (l3 != INT32_MIN) RS_LEAF4(l3);
+#else
+    while (true) {
+        int code;
+        if (l0 != INT32_MIN) { code = l0; l0 = INT32_MIN; }
+        else if (l1 != INT32_MIN) { code = l1; l1 = INT32_MIN; }
+        else if (l2 != INT32_MIN) { code = l2; l2 = INT32_MIN; }
+        else if (l3 != INT32_MIN) { code = l3; l3 = INT32_MIN; }
+        else break;
+        RS_LEAF4(code);
+    }
+#endif
+    return next;
+#undef RS_LEAF4
+#undef RS_ST_LEAF4
+}
+
+template <int SM>
+__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk);
+template <int SM>
+__device__ __noinline__ int traverse_call(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
+    return traverse_body<SM>(S, r, tmin, bend_out, stk);
+}
+// inlined into the kernels of every scene mode but the generic one (a real call makes the kernel
+// keep its live registers in scratch across it: the nest-2 extend spilled 1.2 KB per lane)
+template <int SM>
+__device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
+    if constexpr (SM == kSmGeneric) return traverse_call<SM>(S, r, tmin, bend_out, stk);
+    else return traverse_body<SM>(S, r, tmin, bend_out, stk);
+}
+template <int SM>
+__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
     if (S.root < 0) return -1;
     const RayC rc = ray_consts(r);
     const RayF rf = make_rayf(r.o, rc.inv);
@@ -303,6 +452,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
 #define RS_ST_NODE()
 #define RS_ST_LEAF()
 #endif
+// a leaf: child code ~e names leaf entry e (rs_layout.h)
 #define RS_LEAF(code)                                                          \
     do {                                                                       \
         RS_ST_LEAF();                                                          \
@@ -311,89 +461,13 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
     if (S.root4 >= 0) {
-        // 4-wide near-first: test the four child boxes of one 128-byte node, leaves at once, inner
-        // children ordered by entry distance (nearest next, the rest pushed far-to-near).
-        node = S.root4;
+        // 4-wide near-first (bvh4_step): nearest inner child next, the rest pushed far-to-near
         const RayF4 rq = make_rayf4(rf);
-        float4 NX, FX, NY, FY, NZ, FZ;
-        int4 NC;
-#define RS_FETCH4(nd)                                                                         \
-        {                                                                                     \
-            const char* nb = (const char*)(S.nodes4 + (nd));                                  \
-            NX = *(const float4*)(nb + rq.noff[0]); FX = *(const float4*)(nb + far_off(rq.noff[0], 0)); \
-            NY = *(const float4*)(nb + rq.noff[1]); FY = *(const float4*)(nb + far_off(rq.noff[1], 1)); \
-            NZ = *(const float4*)(nb + rq.noff[2]); FZ = *(const float4*)(nb + far_off(rq.noff[2], 2)); \
-            NC = *(const int4*)(nb + 96);                                                     \
-        }
-        while (true) {
+        node = S.root4;
+        while (node >= 0) {
             RS_ST_NODE();
-            RS_FETCH4(node);
-            // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
-            // and tested after the four box tests, when the node's registers are dead. Branch-free:
-            // all four boxes are tested (the node's loads issue together) and the slot results are
-            // selects; an empty slot (INT32_MIN) is neither a leaf nor an inner child.
-            int n0, n1, n2, n3, l0, l1, l2, l3;
-            float e0, e1, e2, e3;
-#define RS_SLOT(K, NK, EK, LK)                                                                \
-            {                                                                                 \
-                float e;                                                                      \
-                const int c = NC.K;                                                           \
-                const bool hk = slab4(NX.K, NY.K, NZ.K, FX.K, FY.K, FZ.K, rq, tmin32, best32, e) & (c != INT32_MIN); \
-                LK = (hk & (c < 0)) ? c : INT32_MIN;                                          \
-                NK = c;                                                                       \
-                EK = (hk & (c >= 0)) ? e : -__builtin_huge_valf();                            \
-            }
-            RS_SLOT(x, n0, e0, l0) RS_SLOT(y, n1, e1, l1) RS_SLOT(z, n2, e2, l2) RS_SLOT(w, n3, e3, l3)
-#undef RS_SLOT
-            const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
-                            (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
-            int next;
-            if (cnt == 0) {
-                next = -1;
-                if (sp > 0) { --sp; next = stk.get(sp); }
-            } else {
-                // sort descending by entry (farthest first, not-visited last): 5 compare-swaps
-#define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
-                RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
-#undef RS_CS
-                // the cnt - 1 farther children are pushed; inside the LDS part all three writes are
-                // issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
-                if (sp + 3 <= kStackMax) {
-                    stk.lds[sp * kBlock] = n0;
-                    stk.lds[(sp + 1) * kBlock] = n1;
-                    stk.lds[(sp + 2) * kBlock] = n2;
-                } else {
-                    if (cnt > 1) stk.put(sp, n0);
-                    if (cnt > 2) stk.put(sp + 1, n1);
-                    if (cnt > 3) stk.put(sp + 2, n2);
-                }
-                sp += cnt - 1;
-                next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
-            }
-            // leaves of this node (their hits only shrink the range the next node is tested with),
-            // in slot order through ONE copy of the leaf test: every lane tests its k-th leaf in
-            // the same pass, so a wave runs max-over-lanes leaf tests per node, not one pass per
-            // slot that any lane uses
-#ifdef RS_LEAF_PER_SLOT
-            if (l0 != INT32_MIN) RS_LEAF(l0);
-            if (l1 != INT32_MIN) RS_LEAF(l1);
-            if (l2 != INT32_MIN) RS_LEAF(l2);
-            if (l3 != INT32_MIN) RS_LEAF(l3);
-#else
-            while (true) {
-                int code;
-                if (l0 != INT32_MIN) { code = l0; l0 = INT32_MIN; }
-                else if (l1 != INT32_MIN) { code = l1; l1 = INT32_MIN; }
-                else if (l2 != INT32_MIN) { code = l2; l2 = INT32_MIN; }
-                else if (l3 != INT32_MIN) { code = l3; l3 = INT32_MIN; }
-                else break;
-                RS_LEAF(code);
-            }
-#endif
-            if (next < 0) break;
-            node = next;
+            node = bvh4_step<SM>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
         }
-#undef RS_FETCH4
     } else if ((SM == kSmSpheres) || !S.ref_order) {
         while (true) {
             const DNode N = S.nodes[node];
@@ -459,7 +533,7 @@ __device__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend
     s_st_leaves[threadIdx.x] = st_leaves;
 #endif
     bend_out = bend;
-    return bp;
+    return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
 // Recompute the full record of the winner with the exact range it was accepted under.
@@ -647,8 +721,9 @@ __device__ V3 trace_path(const DScene& S, Ray ray, uint32_t depth, Rng& rng, con
 }
 
 template <int SM>
-__global__ __launch_bounds__(kBlock) void k_path_mega(DScene S, DCamera C, PathParams P, double* __restrict__ rad,
+__global__ __launch_bounds__(kBlock) void k_path_mega(const DScene* __restrict__ Sp, DCamera C, PathParams P, double* __restrict__ rad,
                                                       unsigned long long* __restrict__ seg_counters) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const Stk stk = make_stk(S, stk_all);
     uint32_t segs = 0;
@@ -824,7 +899,8 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
 #define RS_WF_EXT_FLAT_WAVES 5  // flat scenes (meshes) are traversal-latency bound: keep 5 waves/SIMD
 #endif
 template <int SM>
-__global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) void k_wf_extend(DScene S, WfState W, uint32_t bounce) {
+__global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) void k_wf_extend(const DScene* __restrict__ Sp, WfState W, uint32_t bounce) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const Stk stk = make_stk(S, stk_all);
     const uint32_t n = W.counts[bounce];
@@ -844,9 +920,83 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) v
     }
 }
 
+// Persistent-lane extend for flat scenes (meshes): every lane walks its own sequence of rays
+// i, i + G, i + 2G, ... (G = grid threads) and starts the next one as soon as its current traversal
+// ends, instead of the wave stepping through rays in lock-step (where a wave runs its slowest lane's
+// traversal: on the C5 mesh the mean ray visits 42 % of its wave's node steps). The next ray's
+// records are prefetched into registers when a ray starts, so a refill waits for nothing; the f32
+// ray setup takes the f32 reciprocal of the direction (its error is far inside slab4's 2^-18 slack)
+// and the exact f64 constants are recomputed only for the rare accepted candidates (test_leaf).
+#ifndef RS_WF_PL_WAVES
+#define RS_WF_PL_WAVES 4
+#endif
+__device__ __forceinline__ RayF make_rayf_f32(const V3& o, const V3& d) {
+    RayF r;
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float of = (float)oo[k];
+        const float dk = fabsf(of) * 0x1p-20f + 0x1p-100f;
+        const float iv = fminf(fmaxf(1.0f / (float)dd[k], -1e30f), 1e30f);
+        r.inv[k] = iv;
+        r.opi[k] = (of + dk) * iv;
+        r.omi[k] = (of - dk) * iv;
+    }
+    return r;
+}
 template <int SM>
-__global__ __launch_bounds__(kBlock) void k_wf_shade(DScene S, WfState W, uint32_t bounce, uint32_t depth,
+__global__ __launch_bounds__(kBlock, RS_WF_PL_WAVES) void k_wf_extend_pl(const DScene* __restrict__ Sp, WfState W, uint32_t bounce) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
+    __shared__ int stk_all[kStackMax * kBlock];
+    const Stk stk = make_stk(S, stk_all);
+    const uint32_t n = W.counts[bounce];
+    const WfSet& cur = W.set[bounce & 1];
+    const uint32_t G = gridDim.x * kBlock;
+    const double tmin = 0.0001;
+    const float tmin32 = -round_up_f(-tmin);
+    uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    bool have = i < n;
+    D4 pa, pb;  // prefetched ray_o / ray_d records of ray i
+    if (have) { pa = cur.ray_o[i]; pb = cur.ray_d[i]; }
+    bool fresh = have;
+    Ray r;
+    RayF4 rq;
+    const RayC rc{};  // flat scenes' leaf tests recompute the f64 constants they need
+    int node = -1, sp = 0, bp = -1;
+    double best = RS_INF, bend = RS_INF;
+    float best32 = __builtin_huge_valf();
+#ifdef RS_TRAV_STATS
+    int st_leaves = 0;
+#endif
+    while (true) {
+        if (fresh) {  // start ray i from the prefetched records, prefetch ray i + G
+            r.o = v3(pa.x, pa.y, pa.z); r.time = pa.w;
+            r.d = v3(pb.x, pb.y, pb.z);
+            r.key = 0;
+            rq = make_rayf4(make_rayf_f32(r.o, r.d));
+            node = S.root4; sp = 0; bp = -1;
+            best = RS_INF; bend = RS_INF; best32 = __builtin_huge_valf();
+            fresh = false;
+            const uint32_t j = i + G;
+            if (j < n) { pa = cur.ray_o[j]; pb = cur.ray_d[j]; }
+        }
+        if (have) {
+            node = bvh4_step<SM>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
+            if (node < 0) {  // traversal of ray i complete: World::hit's winner and its range end
+                W.hit[i] = make_double2(__longlong_as_double((long long)(bp >= 0 ? S.lprim[bp] : -1)), bend);
+                i += G;
+                have = i < n;
+                fresh = have;
+            }
+        }
+        if (__ballot(have) == 0ull) break;
+    }
+}
+
+template <int SM>
+__global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ Sp, WfState W, uint32_t bounce, uint32_t depth,
                                                     uint64_t n_items, double* __restrict__ rad) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
     const WfSet& nxt = W.set[(bounce + 1) & 1];
@@ -892,10 +1042,11 @@ constexpr int kClsLight = 6;
 // straight from registers, and only the paths that go on to shading are written (at index i, with
 // T = 1 and L = 0 implied for the bounce-0 shade kernels).
 template <bool GEN, int SM>
-__global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(DScene S, WfState W, uint32_t* const* __restrict__ queues,
+__global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const Stk stk = make_stk(S, stk_all);
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
@@ -1004,9 +1155,10 @@ __device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
 #define RS_LAMB_MIN_WAVES 4  // 130 -> 128 VGPRs (4 waves/SIMD, 12 B spill): 10.01 -> 9.94 ms bench frame
 #endif
 template <int KIND, int SM>
-__global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest2) ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(DScene S, WfState W, const uint32_t* __restrict__ queue,
+__global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest2) ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(const DScene* __restrict__ Sp, WfState W, const uint32_t* __restrict__ queue,
                                                      int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
                                                      uint64_t n_items, double* __restrict__ rad) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
     uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
     const uint32_t n = cnt[1 + cls];
@@ -1151,6 +1303,14 @@ __global__ __launch_bounds__(kBlock) void k_noise(const float4* __restrict__ px,
     if (threadIdx.x == 0 && s_cnt) atomicAdd(count, (unsigned long long)s_cnt);
 }
 
+// RS_PL=1: the persistent-lane flat extend (k_wf_extend_pl) instead of the lock-step one. Measured
+// slower on the C5 mesh (59.0 vs 49.7 ms at 960x540x16, interior-only rays 297 vs 235 ms): the lanes'
+// divergence is inside each node step (leaf tests), not in finished lanes waiting for the wave.
+static bool getenv_flag_no_pl() {
+    static const int v = [] { const char* e = std::getenv("RS_PL"); return e && *e && *e != '0' ? 0 : 1; }();
+    return v != 0;
+}
+
 hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st) {
     const uint64_t blocks = (n + kBlock - 1) / kBlock;
     if (!blocks) return hipSuccess;
@@ -1171,8 +1331,9 @@ hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, u
 
 // Diagnostic: World::hit for a batch of rays (tests/ per-primitive parity probes).
 // rays[i] = o(3) d(3) time; out[i] = hit t1 t2 p(3) n(3) 0 0 outside mat  (13 doubles, oracle layout)
-__global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __restrict__ rays, uint32_t n, double tmin,
+__global__ __launch_bounds__(kBlock) void k_probe_hit(const DScene* __restrict__ Sp, const double* __restrict__ rays, uint32_t n, double tmin,
                                                      double tmax, double* __restrict__ out) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -1192,19 +1353,20 @@ __global__ __launch_bounds__(kBlock) void k_probe_hit(DScene S, const double* __
     }
 }
 
-hipError_t launch_probe_hit(const DScene& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
+hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
                             hipStream_t st) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     if (!blocks) return hipSuccess;
-    hipLaunchKernelGGL(k_probe_hit, dim3(blocks), dim3(kBlock), 0, st, s, rays, n, tmin, tmax, out);
+    hipLaunchKernelGGL(k_probe_hit, dim3(blocks), dim3(kBlock), 0, st, s.dev, rays, n, tmin, tmax, out);
     return hipGetLastError();
 }
 
 // Diagnostic: the radiance and world.hit count of samples s0 .. s0+n-1 of pixel (x, y), each
 // through the megakernel's trace_path (tests/ per-sample parity; the oracle's orc_sample_radiance).
 template <int SM>
-__global__ __launch_bounds__(kBlock) void k_probe_sample(DScene S, DCamera C, PathParams P, uint32_t x, uint32_t y,
+__global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restrict__ Sp, DCamera C, PathParams P, uint32_t x, uint32_t y,
                                                         uint32_t s0, uint32_t n, double* __restrict__ out) {
+    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -1217,19 +1379,19 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(DScene S, DCamera C, Pa
     out[4 * (size_t)i + 3] = (double)segs;
 }
 
-hipError_t launch_probe_sample(const DScene& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
+hipError_t launch_probe_sample(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
                                uint32_t s0, uint32_t n, double* out, hipStream_t st) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     if (!blocks) return hipSuccess;
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_probe_sample<SMC>, dim3(blocks), dim3(kBlock), 0, st, s, c, p, x, y, s0, n, out));
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_probe_sample<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, c, p, x, y, s0, n, out));
     return hipGetLastError();
 }
 
-hipError_t launch_path_mega(const DScene& s, const DCamera& c, const PathParams& p, int sm, double* rad,
+hipError_t launch_path_mega(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, double* rad,
                             unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st) {
     const uint64_t blocks = std::min<uint64_t>((p.n_items + kBlock - 1) / kBlock, max_blocks);
     if (blocks == 0) return hipSuccess;
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_path_mega<SMC>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s, c, p, rad,
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_path_mega<SMC>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s.dev, c, p, rad,
                                           seg_counters));
     return hipGetLastError();
 }
@@ -1242,47 +1404,51 @@ hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w
     return hipGetLastError();
 }
 
-hipError_t launch_wf_extend(const DScene& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st) {
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce));
+hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st) {
+    if (sm == kSmFlat && s.host->root4 >= 0 && !getenv_flag_no_pl()) {
+        hipLaunchKernelGGL(k_wf_extend_pl<kSmFlat>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce);
+        return hipGetLastError();
+    }
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce));
     return hipGetLastError();
 }
 
-hipError_t launch_wf_shade(const DScene& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
+hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st) {
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_shade<SMC>, dim3(blocks), dim3(kBlock), 0, st, s, w, bounce, depth, n_items, rad));
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_shade<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, depth, n_items, rad));
     return hipGetLastError();
 }
 
-hipError_t launch_wfs_extend(const DScene& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
+hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<false, SMC>), dim3(blocks), dim3(kBlock), 0, st, s, w, queues,
+    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<false, SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues,
                                                  bounce, stride, n_items, rad, DCamera{}, PathParams{}, 0ull, 0u));
     return hipGetLastError();
 }
 
-hipError_t launch_wfs_gen_extend(const DScene& s, const DCamera& c, const PathParams& p, const WfState& w,
+hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
                                 uint32_t blocks, int sm, hipStream_t st) {
     if (!blocks) return hipSuccess;
-    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<true, SMC>), dim3(blocks), dim3(kBlock), 0, st, s, w, queues,
+    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<true, SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues,
                                                  0u, stride, p.n_items, rad, c, p, item0, n));
     return hipGetLastError();
 }
 
 template <int SM>
-static void launch_wfs_shade_sm(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+static void launch_wfs_shade_sm(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                                 uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks,
                                 hipStream_t st) {
     switch (cls) {
-    case 0: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_LAMBERTIAN, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 1: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 2: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIFFUSE_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 3: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIELECTRIC, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    default: hipLaunchKernelGGL((k_wfs_shade<-1, SM>), dim3(blocks), dim3(kBlock), 0, st, s, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 0: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_LAMBERTIAN, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 1: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 2: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIFFUSE_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 3: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIELECTRIC, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    default: hipLaunchKernelGGL((k_wfs_shade<-1, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
     }
 }
 
-hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
                            hipStream_t st) {
     RS_SM_SORTED_DISPATCH(sm, launch_wfs_shade_sm<SMC>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st));
@@ -1291,6 +1457,12 @@ hipError_t launch_wfs_shade(const DScene& s, const WfState& w, const uint32_t* q
 
 hipError_t wf_occupancy(int sm, int* e, int* sh) {
     hipError_t r = hipSuccess;
+    if (sm == kSmFlat && !getenv_flag_no_pl()) {
+        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend_pl<kSmFlat>), kBlock, 0);
+        if (r == hipSuccess)
+            r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<kSmFlat>), kBlock, 0);
+        return r;
+    }
     RS_SM_DISPATCH(sm, {
         r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<SMC>), kBlock, 0);
         if (r == hipSuccess)

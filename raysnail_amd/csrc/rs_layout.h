@@ -111,7 +111,10 @@ struct DImage {    // image.rs: 8-bit RGB, row 0 = top, at DScene::tex_u8[off ..
 };
 
 // Binary BVH node: both child boxes live in the parent, so one 64-byte fetch tests two children.
-// child >= 0: inner node index; child < 0: leaf, prim index = ~child; INT32_MIN: empty slot.
+// child >= 0: inner node index; INT32_MIN: empty slot; other child < 0: a leaf. In spheres / flat
+// scenes the leaf holds leaf entry ~child: entries are in tree order (the leaves of a node are
+// adjacent in memory), DScene::lprim maps an entry to its prim handle and lsph / ltri hold what the
+// leaf tests read; in the other scenes ~child is the prim handle itself (lprim null).
 // Boxes are f32 rounded OUTWARD: inner-node tests only cull (conservatively); every leaf is
 // re-tested against the object's exact f64 bbox (DScene::pbox) before the object itself, which
 // is what BVH::hit does with the leaf's own box (bvh.rs:173-177).
@@ -131,6 +134,15 @@ struct alignas(128) DNode4 {
     int32_t pad[4];
 };
 
+// Triangle data in BVH leaf order (flat scenes): what Triangle::hit's accept test reads
+// (triangle_mesh.rs:85-131: p0 and the edges a..f), so a leaf's triangles are contiguous and the
+// traversal needs no DPrim hop; the winner's full record (normals) is rebuilt from DTri.
+struct alignas(16) LTri {
+    double p0[3];
+    double a, b, c, d, e, f;
+    double kind;   // PrimKind of the entry as a double (only PK_TRIANGLE entries carry the fields above)
+};
+
 struct DBox64 {    // an object's reference bbox (exact f64), tested before its hit()
     double lo[3];
     double hi[3];
@@ -143,7 +155,9 @@ struct DScene {
     const uint8_t* pclass;   // per prim handle: wavefront shading class of its material (spheres-only scenes)
     const DPrim* prims;
     const DSphere* spheres;
-    const DSphere* psph;     // spheres-only scenes: the sphere of prim handle p at psph[p] (no DPrim hop)
+    const int32_t* lprim;    // leaf entry -> prim handle (spheres / flat scenes; null: leaf codes are ~prim)
+    const DSphere* lsph;     // spheres-only scenes: the sphere of each leaf entry
+    const LTri* ltri;        // flat scenes: the triangle of each leaf entry (+ every entry's kind)
     const DRect* rects;
     const DBox* boxes;
     const DQuadric* quadrics;
