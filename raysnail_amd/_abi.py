@@ -139,7 +139,9 @@ _LIB = None
 
 
 def lib_path() -> str:
-    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libraysnail_hip.so")
+    # RS_HIP_LIB: a dev variant of the same library (tools/build_variant.sh), e.g. to bisect in tests
+    return os.environ.get("RS_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                        "libraysnail_hip.so")
 
 
 def load() -> C.CDLL:

@@ -783,7 +783,7 @@ void build(rs_scene* s) {
     s->ref_order = !all_monotone;
     Builder B;
     LeafSink leaves;
-    leaves.entries = s->scene_mode == kSmSpheres || s->scene_mode == kSmFlat;
+    leaves.entries = s->scene_mode == kSmFlat;
     B.leaves = &leaves;
     // one object per leaf (measured on the C5 mesh: 2, 4 and 8 objects per leaf were 15 %, 45 % and
     // 100 % slower -- a wave serialises its lanes' longer leaf loops)
@@ -878,9 +878,11 @@ void build(rs_scene* s) {
     // leaf entries in tree order + what each mode's leaf test reads, contiguous per leaf
     stage(s, d.lprim, leaves.prims);
     s->n_leaf_entries = leaves.prims.size();
-    if (s->scene_mode == kSmSpheres) {
-        std::vector<DSphere> lsph(leaves.prims.size());
-        for (size_t e = 0; e < lsph.size(); ++e) lsph[e] = spheres[prims[leaves.prims[e]].idx];
+    if (s->scene_mode == kSmSpheres) {  // prim-indexed sphere copy (leaf codes name prims in this mode)
+        std::vector<DSphere> lsph(s->objs.size());
+        std::memset(lsph.data(), 0, lsph.size() * sizeof(DSphere));
+        for (size_t h = 0; h < s->objs.size(); ++h)
+            if (s->objs[h].kind == PK_SPHERE) lsph[h] = spheres[prims[h].idx];
         stage(s, d.lsph, lsph);
     }
     if (s->scene_mode == kSmFlat) {

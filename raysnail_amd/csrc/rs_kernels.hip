@@ -225,7 +225,7 @@ __device__ __forceinline__ bool flat_hit(const DScene& S, const DPrim& P, const 
 template <int SM>
 __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, const RayC& rc, double tmin, double& best,
                                           double& bend, int& bp) {
-    if (SM == kSmSpheres) {  // leaf-ordered sphere copy: no DPrim hop, a leaf's spheres contiguous
+    if (SM == kSmSpheres) {  // prim-indexed sphere copy: no DPrim hop (e is the prim in this mode)
         test_sphere_leaf(S, S.lsph[e], e, r, rc, tmin, best, bend, bp);
         return;
     }
@@ -468,7 +468,9 @@ __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, doub
             RS_ST_NODE();
             node = bvh4_step<SM>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
         }
-    } else if ((SM == kSmSpheres) || !S.ref_order) {
+    } else if ((SM == kSmSpheres || SM == kSmFlat || SM == kSmGeneric) && !S.ref_order) {
+        // binary near-first (monotone scenes without the 4-wide tree); the nest modes use the
+        // reference order below for these too (valid for any scene, fewer inlined leaf tests)
         while (true) {
             const DNode N = S.nodes[node];
             float e0, e1;
@@ -494,37 +496,30 @@ __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, doub
             }
         }
     } else {
-        bool second = false;  // visiting node's right child (left one already done)
+        // BVH::hit's recursion order (bvh.rs:173-192), one child per pass: k = 0 the left child,
+        // k = 1 the right one (its box tested with the range the left subtree left behind); an inner
+        // left child is entered with the node pushed to come back for its right child. One leaf-test
+        // site, so the nested-object tests are inlined once.
+        int k = 0;
         while (true) {
-            const DNode N = S.nodes[node];
+            const DNode& N = S.nodes[node];
+            const int c = N.child[k];
             float e;
-            if (!second) {
-                const int c0 = N.child[0];
-                if (slab32(N.lo[0], N.hi[0], rf, tmin32, best32, e)) {
-                    if (c0 < 0) {
-                        RS_LEAF(c0);
-                    } else {
-                        stk.put(sp, node);  // come back for the right child
-                        ++sp;
-                        node = c0;
-                        continue;
-                    }
-                }
-            }
-            const int c1 = N.child[1];
-            if (c1 != INT32_MIN && slab32(N.lo[1], N.hi[1], rf, tmin32, best32, e)) {
-                if (c1 < 0) {
-                    RS_LEAF(c1);
+            if (c != INT32_MIN && slab32(N.lo[k], N.hi[k], rf, tmin32, best32, e)) {
+                if (c < 0) {
+                    RS_LEAF(c);
                 } else {
-                    node = c1;
-                    second = false;
+                    if (k == 0) { stk.put(sp, node); ++sp; }  // come back for the right child
+                    node = c;
+                    k = 0;
                     continue;
                 }
             }
+            if (k == 0) { k = 1; continue; }
             if (sp == 0) break;
             --sp;
             node = stk.get(sp);
-            second = true;
+            k = 1;
         }
     }
 #undef RS_LEAF
@@ -1038,11 +1033,17 @@ constexpr int kClsLight = 6;
 #ifndef RS_EXT_MIN_WAVES
 #define RS_EXT_MIN_WAVES 1  // 5 forces <=96 VGPRs but spills; measured slower (14.5 vs 13.8 ms)
 #endif
+#ifndef RS_EXT_MIN_WAVES_N2
+#define RS_EXT_MIN_WAVES_N2 1  // nest-2 scenes (CSG of transforms: C4); 3 spills: 56 -> 79 ms on quadric.sdl
+#endif
+#ifndef RS_EXT_MIN_WAVES_N0
+#define RS_EXT_MIN_WAVES_N0 4  // nest-0 scenes (boxes, quadrics: C2): 129 -> 128 VGPRs, example.sdl 10.8 -> 10.3 ms
+#endif
 // GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
 // straight from registers, and only the paths that go on to shading are written (at index i, with
 // T = 1 and L = 0 implied for the bounce-0 shade kernels).
 template <bool GEN, int SM>
-__global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
+__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
@@ -1089,8 +1090,18 @@ __global__ __launch_bounds__(kBlock, RS_EXT_MIN_WAVES) void k_wfs_extend(const D
                             sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
                             mi = Pr.mat;
                         } else {
-                            finish_hit<SM>(S, bp, r, 0.0001, bend, h);
-                            mi = h.mat;
+                            // emission reads the record's material and point only: for a leaf object
+                            // (a light class is only given to leaf objects and TfFacades of them) from
+                            // its t-only test, without inlining the nested-object code a second time
+                            if (S.prims[bp].kind != PK_XFORM) {
+                                HitT ht;
+                                Obj<0, 0>::hit_t(S, bp, r, 0.0001, bend, ht);
+                                h.p = ht.p;
+                                mi = S.prims[bp].mat;
+                            } else {
+                                finish_hit<SM>(S, bp, r, 0.0001, bend, h);
+                                mi = h.mat;
+                            }
                         }
                         add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
                         cls = -1;

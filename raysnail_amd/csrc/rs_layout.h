@@ -111,10 +111,10 @@ struct DImage {    // image.rs: 8-bit RGB, row 0 = top, at DScene::tex_u8[off ..
 };
 
 // Binary BVH node: both child boxes live in the parent, so one 64-byte fetch tests two children.
-// child >= 0: inner node index; INT32_MIN: empty slot; other child < 0: a leaf. In spheres / flat
-// scenes the leaf holds leaf entry ~child: entries are in tree order (the leaves of a node are
-// adjacent in memory), DScene::lprim maps an entry to its prim handle and lsph / ltri hold what the
-// leaf tests read; in the other scenes ~child is the prim handle itself (lprim null).
+// child >= 0: inner node index; INT32_MIN: empty slot; other child < 0: a leaf. In flat scenes
+// (meshes) the leaf holds leaf entry ~child: entries are in tree order (the leaves of a node are
+// adjacent in memory), DScene::lprim maps an entry to its prim handle and ltri holds what the leaf
+// test reads; in the other scenes ~child is the prim handle itself (lprim null).
 // Boxes are f32 rounded OUTWARD: inner-node tests only cull (conservatively); every leaf is
 // re-tested against the object's exact f64 bbox (DScene::pbox) before the object itself, which
 // is what BVH::hit does with the leaf's own box (bvh.rs:173-177).
@@ -155,8 +155,8 @@ struct DScene {
     const uint8_t* pclass;   // per prim handle: wavefront shading class of its material (spheres-only scenes)
     const DPrim* prims;
     const DSphere* spheres;
-    const int32_t* lprim;    // leaf entry -> prim handle (spheres / flat scenes; null: leaf codes are ~prim)
-    const DSphere* lsph;     // spheres-only scenes: the sphere of each leaf entry
+    const int32_t* lprim;    // leaf entry -> prim handle (flat scenes; null: leaf codes are ~prim)
+    const DSphere* lsph;     // spheres-only scenes: the sphere of prim handle p at lsph[p] (no DPrim hop)
     const LTri* ltri;        // flat scenes: the triangle of each leaf entry (+ every entry's kind)
     const DRect* rects;
     const DBox* boxes;
