@@ -1,6 +1,6 @@
 """Measure BASELINE.json's configs C2-C5 on one GPU (the bench line itself is C1-shaped, bench.py):
 one full frame each after a warm-up frame, plus the CPU oracle on a bounded row subset of the same
-frame (16 threads), scaled by samples. Writes one JSON object per config to stdout.
+frame (num_cpus + 1 threads like Painter::draw), scaled by samples. Writes one JSON object per config to stdout.
 
 usage: python tools/bench_configs.py [--only C3,C4] [--cpu-seconds 10]
 """
@@ -37,7 +37,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=len(os.sched_getaffinity(0)) + 1,
+                    help="default num_cpus + 1 like Painter::draw (painter.rs:321-325)")
     ap.add_argument("--mode", type=int, default=0)
     args = ap.parse_args()
     import torch
