@@ -431,46 +431,12 @@ template <int L, int R> struct Obj {
             if (!tri_t(S.tris[P.idx], r, tmin, tmax, h.t1)) return false;
             h.t2 = RS_FMAX; h.p = ray_at(r, h.t1);
             return true;
-        case PK_AND: {  // csg/intersection.rs:58-100
-            const DCsg C = S.csgs[P.idx];
-            HitT h1, h2;
-            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, h1)) return false;
-            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, h2)) return false;
-            const bool first1 = h1.t1 < h2.t1;
-            const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
-            const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
-            if (Obj<L - 1, R>::contains(S, o1, p0)) h = first1 ? h1 : h2;
-            else if (Obj<L - 1, R>::contains(S, o0, p1)) h = first1 ? h2 : h1;
-            else return false;
-            return true;
-        }
-        case PK_SUB: {  // csg/difference.rs:57-106
-            const DCsg C = S.csgs[P.idx];
-            HitT hp, hm;
-            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, hp)) return false;
-            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, hm)) { h = hp; return true; }
-            if (hp.t1 < hm.t1) {
-                if (Obj<L - 1, R>::contains(S, C.b, hp.p)) return false;
-                h = hp;
-            } else if (hm.t2 < hp.t1) {
-                h = hp;
-            } else if (hm.t2 < hp.t2) {
-                h.p = ray_at(r, hm.t2); h.t1 = hm.t2; h.t2 = hp.t2;
-            } else {
-                return false;
-            }
-            return true;
-        }
-        case PK_XFORM: {  // tf_facade.rs:41-55
-            const DXform X = S.xforms[P.idx];
-            Ray rr;
-            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
-            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
-            rr.time = r.time;
-            if (R) rr.key = r.key;
-            if (!Obj<L - 1, R>::hit_t(S, X.child, rr, tmin, tmax, h)) return false;
-            h.p = tf_forward(S, X, P.aux, h.p, 1.0);
-            return true;
+        case PK_AND:    // csg/intersection.rs:58-100
+        case PK_SUB:    // csg/difference.rs:57-106
+        case PK_XFORM:  // tf_facade.rs:41-55
+        {
+            int wk;
+            return composite_t(S, P, r, tmin, tmax, h, wk);
         }
         case PK_MEDIUM: {  // the record is cheap; reuse it (rich scene mode only)
             if (!R) return false;
@@ -481,6 +447,93 @@ template <int L, int R> struct Obj {
         }
         }
         return false;
+    }
+
+    // CSG and TfFacade decisions through ONE call site of the level below per kind of query: the
+    // children are visited by a loop that is not unrolled. Inlining the object switch once per child
+    // and per level made the nest-2 extend kernel 397 KB of code, far past the instruction cache.
+    // wk: whose record h is -- 0 the first child (Intersection / Difference: a; TfFacade: its child),
+    // 1 the second (b), 2 Difference's synthesized back-face hit of b
+    static __device__ __forceinline__ bool composite_t(const DScene& S, const DPrim& P, const Ray& r, double tmin,
+                                                       double tmax, HitT& h, int& wk) {
+        wk = 0;
+        const bool xf = P.kind == PK_XFORM;
+        int c0, c1 = -1;
+        Ray rr = r;
+        DXform X;
+        if (xf) {
+            X = S.xforms[P.idx];
+            c0 = X.child;
+            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
+            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
+        } else {
+            const DCsg C = S.csgs[P.idx];
+            c0 = C.a;
+            c1 = C.b;
+        }
+        HitT h1, h2;
+        bool ok2 = false;
+#pragma clang loop unroll(disable)
+        for (int k = 0; k < 2; ++k) {
+            HitT t;
+            const bool ok = Obj<L - 1, R>::hit_t(S, k ? c1 : c0, rr, tmin, tmax, t);
+            if (k == 0) {
+                if (!ok) return false;
+                h1 = t;
+                if (xf) break;
+            } else {
+                ok2 = ok;
+                h2 = t;
+            }
+        }
+        if (xf) {
+            h = h1;
+            h.p = tf_forward(S, X, P.aux, h1.p, 1.0);
+            return true;
+        }
+        // the contains() queries, first match wins: Intersection asks (o1, p0) then (o0, p1);
+        // Difference asks (b, hp.p) when its plus hit comes first
+        int q0 = -1, q1 = -1;
+        V3 qp0 = h1.p, qp1 = h1.p;
+        bool first1 = false;
+        if (P.kind == PK_AND) {
+            if (!ok2) return false;
+            first1 = h1.t1 < h2.t1;
+            q0 = first1 ? c1 : c0;       // o1
+            q1 = first1 ? c0 : c1;       // o0
+            qp0 = first1 ? h1.p : h2.p;  // p0
+            qp1 = first1 ? h2.p : h1.p;  // p1
+        } else {
+            if (!ok2) { h = h1; return true; }
+            if (h1.t1 < h2.t1) {
+                q0 = c1;
+            } else if (h2.t2 < h1.t1) {
+                h = h1;
+                return true;
+            } else if (h2.t2 < h1.t2) {
+                h.p = ray_at(r, h2.t2); h.t1 = h2.t2; h.t2 = h1.t2;
+                wk = 2;
+                return true;
+            } else {
+                return false;
+            }
+        }
+        int win = -1;
+#pragma clang loop unroll(disable)
+        for (int k = 0; k < 2; ++k) {
+            const int q = k ? q1 : q0;
+            if (q < 0) break;
+            if (Obj<L - 1, R>::contains(S, q, k ? qp1 : qp0)) { win = k; break; }
+        }
+        if (P.kind == PK_AND) {
+            if (win < 0) return false;
+            wk = ((win == 0) == first1) ? 0 : 1;  // (o1 contains p0): the first hit, else the second
+            h = wk == 0 ? h1 : h2;
+            return true;
+        }
+        if (win >= 0) return false;  // Difference: the plus hit lies inside the minus object
+        h = h1;
+        return true;
     }
 
     static __device__ bool hit(const DScene& S, int pi, const Ray& r, double tmin, double tmax, Hit& h) {
@@ -494,54 +547,40 @@ template <int L, int R> struct Obj {
         case PK_BOX: return box_hit(S.boxes[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         case PK_QUADRIC: return quadric_hit(S.quadrics[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
         case PK_TRIANGLE: return tri_hit(S.tris[P.idx], P.mat, r, tmin, tmax, h, R ? S.uv : 0);
-        case PK_AND: {  // csg/intersection.rs:58-100: decided on (t1, t2, p), then the winner's record
-            const DCsg C = S.csgs[P.idx];
-            HitT h1, h2;
-            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, h1)) return false;
-            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, h2)) return false;
-            const bool first1 = h1.t1 < h2.t1;
-            const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
-            const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
-            int win;
-            if (Obj<L - 1, R>::contains(S, o1, p0)) win = o0;
-            else if (Obj<L - 1, R>::contains(S, o0, p1)) win = o1;
-            else return false;
-            Obj<L - 1, R>::hit(S, win, r, tmin, tmax, h);
-            if (h.mat < 0) h.mat = P.mat;  // set_material_if_none (hit.rs:69-78)
-            return true;
-        }
-        case PK_SUB: {  // csg/difference.rs:57-106
-            const DCsg C = S.csgs[P.idx];
-            HitT hp, hm;
-            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, hp)) return false;
-            bool plus;
-            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, hm)) plus = true;
-            else if (hp.t1 < hm.t1) {
-                if (Obj<L - 1, R>::contains(S, C.b, hp.p)) return false;
-                plus = true;
-            } else plus = hm.t2 < hp.t1;
-            if (plus) {
-                Obj<L - 1, R>::hit(S, C.a, r, tmin, tmax, h);
-            } else if (hm.t2 < hp.t2) {
-                V3 p = ray_at(r, hm.t2);
-                V3 n = shape_normal(S, C.b, p);
-                h.p = p; h.n = -n; h.mat = S.prims[C.b].mat; h.t1 = hm.t2; h.t2 = hp.t2; h.outside = 1;
-                if (R) { h.u = 0.0; h.v = 0.0; }
-            } else {
-                return false;
-            }
-            if (h.mat < 0) h.mat = P.mat;
-            return true;
-        }
+        case PK_AND:      // csg/intersection.rs:58-100: decided on (t1, t2, p), then the winner's record
+        case PK_SUB:      // csg/difference.rs:57-106
         case PK_XFORM: {  // tf_facade.rs:41-55 (normal stays in object space, t unchanged)
-            const DXform X = S.xforms[P.idx];
-            Ray rr;
-            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
-            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
-            rr.time = r.time;
-            if (R) rr.key = r.key;
-            if (!Obj<L - 1, R>::hit(S, X.child, rr, tmin, tmax, h)) return false;
-            h.p = tf_forward(S, X, P.aux, h.p, 1.0);
+            const bool xf = P.kind == PK_XFORM;
+            int child;
+            Ray rr = r;
+            DXform X;
+            if (xf) {
+                X = S.xforms[P.idx];
+                child = X.child;
+                rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
+                rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
+            } else {
+                HitT t;
+                int wk;
+                if (!composite_t(S, P, r, tmin, tmax, t, wk)) return false;
+                const DCsg C = S.csgs[P.idx];
+                if (wk == 2) {  // Difference: the minus object's far hit, facing out of the plus one
+                    const V3 n = shape_normal(S, C.b, t.p);
+                    h.p = t.p; h.n = -n; h.mat = S.prims[C.b].mat; h.t1 = t.t1; h.t2 = t.t2; h.outside = 1;
+                    if (R) { h.u = 0.0; h.v = 0.0; }
+                    if (h.mat < 0) h.mat = P.mat;
+                    return true;
+                }
+                child = wk ? C.b : C.a;
+            }
+            // the winner's own record (one call site of the level below)
+            const bool ok = Obj<L - 1, R>::hit(S, child, rr, tmin, tmax, h);
+            if (xf) {
+                if (!ok) return false;
+                h.p = tf_forward(S, X, P.aux, h.p, 1.0);
+                return true;
+            }
+            if (h.mat < 0) h.mat = P.mat;  // set_material_if_none (hit.rs:69-78)
             return true;
         }
         case PK_MEDIUM: {  // medium/constant.rs:42-84
@@ -584,11 +623,33 @@ template <int L, int R> struct Obj {
         }
         case PK_BOX: return box_contains(S.boxes[P.idx], p);
         case PK_QUADRIC: return quadric_contains(S.quadrics[P.idx], p);
-        case PK_AND: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1, R>::contains(S, C.a, p) && Obj<L - 1, R>::contains(S, C.b, p); }
-        case PK_SUB: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1, R>::contains(S, C.a, p) && !Obj<L - 1, R>::contains(S, C.b, p); }
-        case PK_XFORM: {
-            const DXform X = S.xforms[P.idx];
-            return Obj<L - 1, R>::contains(S, X.child, tf_inverse(S, X, P.aux, p, 1.0));
+        case PK_AND:    // a && b
+        case PK_SUB:    // a && !b
+        case PK_XFORM: {  // child at the inverse-transformed point
+            // one call site of the level below (loop not unrolled), as in composite_t
+            const bool xf = P.kind == PK_XFORM;
+            int c0, c1 = -1;
+            V3 q = p;
+            if (xf) {
+                const DXform X = S.xforms[P.idx];
+                c0 = X.child;
+                q = tf_inverse(S, X, P.aux, p, 1.0);
+            } else {
+                const DCsg C = S.csgs[P.idx];
+                c0 = C.a;
+                c1 = C.b;
+            }
+#pragma clang loop unroll(disable)
+            for (int k = 0; k < 2; ++k) {
+                const bool in = Obj<L - 1, R>::contains(S, k ? c1 : c0, q);
+                if (k == 0) {
+                    if (xf) return in;
+                    if (!in) return false;
+                } else {
+                    return P.kind == PK_AND ? in : !in;
+                }
+            }
+            return false;
         }
         default: return false;  // AARect / Triangle: false; ConstantMedium: unimplemented! upstream (constant.rs:86-91)
         }

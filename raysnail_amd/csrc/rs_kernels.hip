@@ -873,6 +873,13 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
     camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
     return true;
 }
+// The camera ray and stream state of a live item again (the bounce-0 shading kernels recompute them
+// instead of reading a path record that bounce 0 would have had to write: 100 B per path each way)
+__device__ __forceinline__ void camera_regen(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
+    const uint32_t pl = (uint32_t)(item % P.n_pix_local);
+    const uint32_t sl = (uint32_t)(item / P.n_pix_local);
+    camera_sample_xy(C, P, pl % P.width, P.row_begin + (pl / P.width) * P.row_step, P.s0 + sl, r, rng);
+}
 
 __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfState W, uint64_t item0, uint32_t n,
                                                    double* __restrict__ rad) {
@@ -1039,11 +1046,71 @@ constexpr int kClsLight = 6;
 #ifndef RS_EXT_MIN_WAVES_N0
 #define RS_EXT_MIN_WAVES_N0 4  // nest-0 scenes (boxes, quadrics: C2): 129 -> 128 VGPRs, example.sdl 10.8 -> 10.3 ms
 #endif
-// GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
-// straight from registers, and only the paths that go on to shading are written (at index i, with
-// T = 1 and L = 0 implied for the bounce-0 shade kernels).
+// Coherence sort of one extend batch (bounces >= 1): records bb .. bb + nb of the path set are
+// counted into direction cells (ext_sort_key) in LDS and s_perm receives their set indices in cell
+// order, so each wave traces rays of one cell (the wave runs the union of its lanes' traversal loops).
+// Pure scheduling: every record is traced once, by a lane of this block, with the same arithmetic.
+#ifndef RS_EXT_SORT_KEY
+#define RS_EXT_SORT_KEY 0  // 0: no sort, 1: direction octant, 2: octant x dominant axis
+#endif
+#ifndef RS_EXT_SORT_R
+#define RS_EXT_SORT_R 4    // records per thread per batch (a batch of R * kBlock is sorted)
+#endif
+constexpr uint32_t kSortCells = 64;
+__device__ __forceinline__ uint32_t ext_sort_key(const D4& d) {
+    const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
+#if RS_EXT_SORT_KEY >= 2
+    const double ax = fabs(d.x), ay = fabs(d.y), az = fabs(d.z);
+    const uint32_t major = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
+    return oct * 3u + major;
+#else
+    return oct;
+#endif
+}
+template <uint32_t R>
+__device__ __forceinline__ void ext_sort_batch(const WfSet& cur, uint32_t cap, uint32_t nf, uint32_t bb, uint32_t nb,
+                                               uint32_t* s_perm) {
+    __shared__ uint32_t s_hist[kSortCells];
+    if (threadIdx.x < kSortCells) s_hist[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t ri[R], rk[R], rn[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t jj = r * kBlock + threadIdx.x;
+        if (jj < nb) {
+            const uint32_t j = bb + jj;
+            ri[r] = j < nf ? j : cap - 1u - (j - nf);
+            rk[r] = ext_sort_key(cur.ray_d[ri[r]]);
+            rn[r] = atomicAdd(&s_hist[rk[r]], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the cell counts (one wave)
+        const uint32_t lane = threadIdx.x, v = lane < kSortCells ? s_hist[lane] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(x, off, 64);
+            if (lane >= (uint32_t)off) x += t;
+        }
+        if (lane < kSortCells) s_hist[lane] = x - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r)
+        if (r * kBlock + threadIdx.x < nb) s_perm[s_hist[rk[r]] + rn[r]] = ri[r];
+    __syncthreads();
+}
+
+// GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i and traverses it
+// straight from registers; for the paths that go on to shading only the hit (16 B) and the queue slot
+// are written -- the bounce-0 shade kernels regenerate ray and stream state from item0 + i, with
+// T = 1 and L = 0 implied.
+#ifndef RS_EXT_MIN_WAVES_SORT
+#define RS_EXT_MIN_WAVES_SORT 4  // spheres, bounces >= 1 (the coherence-sorted batches): 135 -> 127 VGPRs, no spill
+#endif
 template <bool GEN, int SM>
-__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
+__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : GEN ? RS_EXT_MIN_WAVES : RS_EXT_MIN_WAVES_SORT) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
@@ -1055,13 +1122,26 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
     const uint32_t n = GEN ? n_gen : nf + cnt[kCntBack];
     if (!GEN && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n;  // live paths at this bounce (stats)
     const WfSet& cur = W.set[bounce & 1];
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    // bounces >= 1 with a coherence sort: a block takes R * kBlock records per batch and traces them
+    // in direction-cell order (ext_sort_batch), R rounds of kBlock; otherwise one record per thread
+    constexpr bool kSort = !GEN && RS_EXT_SORT_KEY > 0;
+    constexpr uint32_t R = kSort ? RS_EXT_SORT_R : 1u;
+    constexpr uint32_t kBatch = kBlock * R;
+    __shared__ uint32_t s_perm[kSort ? kBatch : 1];
+    for (uint32_t bb = blockIdx.x * kBatch; bb < n; bb += gridDim.x * kBatch) {
+      const uint32_t nb = min(kBatch, n - bb);
+      if constexpr (kSort) ext_sort_batch<R>(cur, W.cap, nf, bb, nb, s_perm);
+      for (uint32_t rr = 0; rr < R; ++rr) {
+        const uint32_t jj = rr * kBlock + threadIdx.x;
+        const bool valid = jj < nb;
         // thread -> record: the front run [0, nf), then the back run from the set's end down
-        const uint32_t j = base + threadIdx.x;
-        const uint32_t i = (GEN || j < nf) ? j : W.cap - 1u - (j - nf);
+        const uint32_t j = bb + jj;
+        uint32_t i;
+        if constexpr (kSort) i = valid ? s_perm[jj] : 0u;
+        else i = (GEN || j < nf) ? j : W.cap - 1u - (j - nf);
         int cls = -1;
         bool live = false;
-        if (j < n) {
+        if (valid) {
             Ray r;
             Rng rng;
             uint32_t item = 0;
@@ -1105,9 +1185,8 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
                         }
                         add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
                         cls = -1;
-                    } else {
+                    } else {  // bounce 0: the shading kernel regenerates the camera ray (camera_regen)
                         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-                        if (GEN) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item);
                         done = false;
                     }
                 }
@@ -1131,6 +1210,7 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
         uint32_t* const cs[kClasses] = {&cnt[1], &cnt[2], &cnt[3], &cnt[4], &cnt[5]};
         const uint32_t slot = block_slot<kClasses>(cls, cs);
         if (cls >= 0) queues[cls][slot] = i;
+      }
     }
 }
 
@@ -1165,10 +1245,13 @@ __device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
 #ifndef RS_LAMB_MIN_WAVES
 #define RS_LAMB_MIN_WAVES 4  // 130 -> 128 VGPRs (4 waves/SIMD, 12 B spill): 10.01 -> 9.94 ms bench frame
 #endif
-template <int KIND, int SM>
+// FIRST = bounce 0: the path is regenerated from its camera sample (item0 + queued index, see
+// k_wfs_extend<true>) instead of being read from a path record.
+template <int KIND, int SM, bool FIRST>
 __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest2) ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(const DScene* __restrict__ Sp, WfState W, const uint32_t* __restrict__ queue,
                                                      int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
-                                                     uint64_t n_items, double* __restrict__ rad) {
+                                                     uint64_t n_items, double* __restrict__ rad, DCamera C,
+                                                     PathParams P, uint64_t item0) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
     uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
@@ -1198,12 +1281,18 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
         uint32_t item = 0;
         if (j < n) {
             const uint32_t i = queue[j];
-            load_path(cur, i, r, T, rng);
+            if (FIRST) {
+                item = (uint32_t)(item0 + i);
+                camera_regen(C, P, item, r, rng);
+                T = v3(1.0, 1.0, 1.0);
+            } else {
+                load_path(cur, i, r, T, rng);
+                item = cur.item[i];
+            }
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
             finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
-            item = cur.item[i];
             const int mi = h.mat >= 0 ? h.mat : S.default_mat;
             const DMaterial& M0 = S.mats[mi];
             bool cont;
@@ -1430,6 +1519,8 @@ hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce,
     return hipGetLastError();
 }
 
+uint32_t wfs_extend_batch() { return RS_EXT_SORT_KEY > 0 ? kBlock * RS_EXT_SORT_R : kBlock; }
+
 hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st) {
     RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<false, SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues,
@@ -1446,23 +1537,32 @@ hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const Path
     return hipGetLastError();
 }
 
-template <int SM>
+template <int SM, bool FIRST>
 static void launch_wfs_shade_sm(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                                 uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks,
-                                hipStream_t st) {
+                                const DCamera& c, const PathParams& p, uint64_t item0, hipStream_t st) {
+#define RS_SHADE_LAUNCH(KIND) \
+    hipLaunchKernelGGL((k_wfs_shade<KIND, SM, FIRST>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, \
+                       stride, depth, n_items, rad, c, p, item0)
     switch (cls) {
-    case 0: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_LAMBERTIAN, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 1: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 2: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIFFUSE_METAL, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    case 3: hipLaunchKernelGGL((k_wfs_shade<RS_MAT_DIELECTRIC, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
-    default: hipLaunchKernelGGL((k_wfs_shade<-1, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, stride, depth, n_items, rad); break;
+    case 0: RS_SHADE_LAUNCH(RS_MAT_LAMBERTIAN); break;
+    case 1: RS_SHADE_LAUNCH(RS_MAT_METAL); break;
+    case 2: RS_SHADE_LAUNCH(RS_MAT_DIFFUSE_METAL); break;
+    case 3: RS_SHADE_LAUNCH(RS_MAT_DIELECTRIC); break;
+    default: RS_SHADE_LAUNCH(-1); break;
     }
+#undef RS_SHADE_LAUNCH
 }
 
 hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
-                           hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, launch_wfs_shade_sm<SMC>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st));
+                           const DCamera& c, const PathParams& p, uint64_t item0, hipStream_t st) {
+    if (bounce == 0)
+        RS_SM_SORTED_DISPATCH(sm, (launch_wfs_shade_sm<SMC, true>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks,
+                                                                 c, p, item0, st)));
+    else
+        RS_SM_SORTED_DISPATCH(sm, (launch_wfs_shade_sm<SMC, false>(s, w, queue, cls, bounce, stride, depth, n_items, rad,
+                                                                  blocks, c, p, item0, st)));
     return hipGetLastError();
 }
 
