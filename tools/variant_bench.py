@@ -21,7 +21,9 @@ print(f"frame {best[0]:.2f} ms extend {best[1]:.2f} ms {st.samples/best[0]/1e3:.
 SCENES = {"rtow": ("scenes.rtow_13_1(800, 500)[:2]", 64, 8),
           "example": ("scenes.example_sdl(800, 500)", 64, 8),
           "quadric": ("scenes.quadric_sdl(512, 512)", 16, 8),
-          "mesh": ("scenes.mesh_scene(480, 270, 64, 120)", 16, 8)}
+          "mesh": ("scenes.mesh_scene(480, 270, 64, 120)", 16, 8),
+          "c4": ("scenes.quadric_sdl(512, 512)", 64, 50),
+          "c5": ("scenes.mesh_scene(960, 540)", 16, 50)}
 
 
 def main():
