@@ -709,12 +709,39 @@ class TakePhotoSettings:
         if pixel_map is not None and type(pixel_map) is not PixelController:
             mask = np.array([[1 if pixel_map.calculate_pixel(x, y) else 0 for x in range(cam.width)]
                              for y in range(cam.height)], dtype=np.uint8)
-        out, stats = world.device_scene().render(cam, self.settings(), mask)
-        self.last_stats = stats
-        if target is not None:
-            for y in range(cam.height):
+        st = self.settings()
+        if target is None:
+            out, stats = world.device_scene().render(cam, st, mask)
+            self.last_stats = stats
+            return out
+        # progressive delivery (painter.rs:214 registers each row as a worker finishes it): the row
+        # lattice in 8 bands, each band's rows handed over when the band is done; pixels do not depend
+        # on the banding (per-sample RNG streams), so the frame equals the one-call frame
+        H = cam.height
+        rb, step = st.row_begin, st.row_step or 1
+        re = min(st.row_end, H) if st.row_end else H
+        rows = list(range(rb, re, step))
+        per = max(1, -(-len(rows) // 8))
+        out = np.zeros((H, cam.width, 4), np.float32)
+        total = A.rs_render_stats()
+        sent = set()
+        for k in range(0, len(rows), per):
+            band = rows[k:k + per]
+            bs = self.settings()
+            bs.row_begin, bs.row_end, bs.row_step = band[0], band[-1] + 1, step
+            img, s = world.device_scene().render(cam, bs, mask)
+            for f in ("samples", "segments", "ms", "path_ms", "launches", "kernel_launches", "kernel_ms", "kernel_bytes"):
+                setattr(total, f, getattr(total, f) + getattr(s, f))
+            total.kernel_id, total.tree_arity = s.kernel_id, s.tree_arity
+            for y in band:
+                out[y] = img[y]
                 target.register_pixels(y, out[y])
-            target.register_pixels(cam.height, [])  # end-of-pass sentinel (painter.rs:332)
+                sent.add(y)
+        for y in range(H):  # rows off the lattice (all zero), once each
+            if y not in sent:
+                target.register_pixels(y, out[y])
+        self.last_stats = total
+        target.register_pixels(H, [])  # end-of-pass sentinel (painter.rs:332)
         return out
 
     def shot(self, path, world: World) -> np.ndarray:

@@ -396,6 +396,9 @@ template <int R> struct Obj<-1, R> {
 };
 
 template <int L, int R> struct Obj {
+    // one call site of the level below per query (composite_t) where the levels are inlined; the
+    // generic / rich mode's levels are calls, which keep the per-child sites (composite_t_calls)
+    static constexpr bool kOneSite = L <= 2 && R == 0;
     // inlined in the scene modes with at most two nesting levels (no call frames and no spills in
     // their traversal loops); the generic mode's up-to-4-level copies stay calls (code size)
     static __device__ __forceinline__ bool hit_t(const DScene& S, int pi, const Ray& r, double tmin, double tmax, HitT& h) {
@@ -434,10 +437,12 @@ template <int L, int R> struct Obj {
         case PK_AND:    // csg/intersection.rs:58-100
         case PK_SUB:    // csg/difference.rs:57-106
         case PK_XFORM:  // tf_facade.rs:41-55
-        {
-            int wk;
-            return composite_t(S, P, r, tmin, tmax, h, wk);
-        }
+            if constexpr (kOneSite) {
+                int wk;
+                return composite_t(S, P, r, tmin, tmax, h, wk);
+            } else {
+                return composite_t_calls(S, P, r, tmin, tmax, h);
+            }
         case PK_MEDIUM: {  // the record is cheap; reuse it (rich scene mode only)
             if (!R) return false;
             Hit f;
@@ -452,6 +457,56 @@ template <int L, int R> struct Obj {
     // CSG and TfFacade decisions through ONE call site of the level below per kind of query: the
     // children are visited by a loop that is not unrolled. Inlining the object switch once per child
     // and per level made the nest-2 extend kernel 397 KB of code, far past the instruction cache.
+    // the calls variant (generic / rich mode, where each level below is a real call): one site per
+    // child, as a loop around a call would keep its state live across the call (X1 / X2 slower)
+    static __device__ __forceinline__ bool composite_t_calls(const DScene& S, const DPrim& P, const Ray& r, double tmin,
+                                                             double tmax, HitT& h) {
+        switch (P.kind) {
+        case PK_AND: {  // csg/intersection.rs:58-100
+            const DCsg C = S.csgs[P.idx];
+            HitT h1, h2;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, h1)) return false;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, h2)) return false;
+            const bool first1 = h1.t1 < h2.t1;
+            const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
+            const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
+            if (Obj<L - 1, R>::contains(S, o1, p0)) h = first1 ? h1 : h2;
+            else if (Obj<L - 1, R>::contains(S, o0, p1)) h = first1 ? h2 : h1;
+            else return false;
+            return true;
+        }
+        case PK_SUB: {  // csg/difference.rs:57-106
+            const DCsg C = S.csgs[P.idx];
+            HitT hp, hm;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, hp)) return false;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, hm)) { h = hp; return true; }
+            if (hp.t1 < hm.t1) {
+                if (Obj<L - 1, R>::contains(S, C.b, hp.p)) return false;
+                h = hp;
+            } else if (hm.t2 < hp.t1) {
+                h = hp;
+            } else if (hm.t2 < hp.t2) {
+                h.p = ray_at(r, hm.t2); h.t1 = hm.t2; h.t2 = hp.t2;
+            } else {
+                return false;
+            }
+            return true;
+        }
+        case PK_XFORM: {  // tf_facade.rs:41-55
+            const DXform X = S.xforms[P.idx];
+            Ray rr;
+            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
+            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
+            rr.time = r.time;
+            if (R) rr.key = r.key;
+            if (!Obj<L - 1, R>::hit_t(S, X.child, rr, tmin, tmax, h)) return false;
+            h.p = tf_forward(S, X, P.aux, h.p, 1.0);
+            return true;
+        }
+        }
+        return false;
+    }
+
     // wk: whose record h is -- 0 the first child (Intersection / Difference: a; TfFacade: its child),
     // 1 the second (b), 2 Difference's synthesized back-face hit of b
     static __device__ __forceinline__ bool composite_t(const DScene& S, const DPrim& P, const Ray& r, double tmin,
@@ -536,6 +591,63 @@ template <int L, int R> struct Obj {
         return true;
     }
 
+    static __device__ __forceinline__ bool composite_hit_calls(const DScene& S, const DPrim& P, const Ray& r, double tmin,
+                                                               double tmax, Hit& h) {
+        switch (P.kind) {
+        case PK_AND: {  // csg/intersection.rs:58-100: decided on (t1, t2, p), then the winner's record
+            const DCsg C = S.csgs[P.idx];
+            HitT h1, h2;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, h1)) return false;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, h2)) return false;
+            const bool first1 = h1.t1 < h2.t1;
+            const int o0 = first1 ? C.a : C.b, o1 = first1 ? C.b : C.a;
+            const V3 p0 = first1 ? h1.p : h2.p, p1 = first1 ? h2.p : h1.p;
+            int win;
+            if (Obj<L - 1, R>::contains(S, o1, p0)) win = o0;
+            else if (Obj<L - 1, R>::contains(S, o0, p1)) win = o1;
+            else return false;
+            Obj<L - 1, R>::hit(S, win, r, tmin, tmax, h);
+            if (h.mat < 0) h.mat = P.mat;  // set_material_if_none (hit.rs:69-78)
+            return true;
+        }
+        case PK_SUB: {  // csg/difference.rs:57-106
+            const DCsg C = S.csgs[P.idx];
+            HitT hp, hm;
+            if (!Obj<L - 1, R>::hit_t(S, C.a, r, tmin, tmax, hp)) return false;
+            bool plus;
+            if (!Obj<L - 1, R>::hit_t(S, C.b, r, tmin, tmax, hm)) plus = true;
+            else if (hp.t1 < hm.t1) {
+                if (Obj<L - 1, R>::contains(S, C.b, hp.p)) return false;
+                plus = true;
+            } else plus = hm.t2 < hp.t1;
+            if (plus) {
+                Obj<L - 1, R>::hit(S, C.a, r, tmin, tmax, h);
+            } else if (hm.t2 < hp.t2) {
+                V3 p = ray_at(r, hm.t2);
+                V3 n = shape_normal(S, C.b, p);
+                h.p = p; h.n = -n; h.mat = S.prims[C.b].mat; h.t1 = hm.t2; h.t2 = hp.t2; h.outside = 1;
+                if (R) { h.u = 0.0; h.v = 0.0; }
+            } else {
+                return false;
+            }
+            if (h.mat < 0) h.mat = P.mat;
+            return true;
+        }
+        case PK_XFORM: {  // tf_facade.rs:41-55 (normal stays in object space, t unchanged)
+            const DXform X = S.xforms[P.idx];
+            Ray rr;
+            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
+            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
+            rr.time = r.time;
+            if (R) rr.key = r.key;
+            if (!Obj<L - 1, R>::hit(S, X.child, rr, tmin, tmax, h)) return false;
+            h.p = tf_forward(S, X, P.aux, h.p, 1.0);
+            return true;
+        }
+        }
+        return false;
+    }
+
     static __device__ bool hit(const DScene& S, int pi, const Ray& r, double tmin, double tmax, Hit& h) {
         const DPrim P = S.prims[pi];
         switch (P.kind) {
@@ -550,6 +662,7 @@ template <int L, int R> struct Obj {
         case PK_AND:      // csg/intersection.rs:58-100: decided on (t1, t2, p), then the winner's record
         case PK_SUB:      // csg/difference.rs:57-106
         case PK_XFORM: {  // tf_facade.rs:41-55 (normal stays in object space, t unchanged)
+            if constexpr (!kOneSite) return composite_hit_calls(S, P, r, tmin, tmax, h);
             const bool xf = P.kind == PK_XFORM;
             int child;
             Ray rr = r;
@@ -613,6 +726,17 @@ template <int L, int R> struct Obj {
         else return contains_call(S, pi, p);
     }
     static __device__ __noinline__ bool contains_call(const DScene& S, int pi, V3 p) { return contains_body(S, pi, p); }
+    static __device__ __forceinline__ bool contains_calls(const DScene& S, const DPrim& P, V3 p) {
+        switch (P.kind) {
+        case PK_AND: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1, R>::contains(S, C.a, p) && Obj<L - 1, R>::contains(S, C.b, p); }
+        case PK_SUB: { const DCsg C = S.csgs[P.idx]; return Obj<L - 1, R>::contains(S, C.a, p) && !Obj<L - 1, R>::contains(S, C.b, p); }
+        case PK_XFORM: {
+            const DXform X = S.xforms[P.idx];
+            return Obj<L - 1, R>::contains(S, X.child, tf_inverse(S, X, P.aux, p, 1.0));
+        }
+        default: return false;
+        }
+    }
     static __device__ __forceinline__ bool contains_body(const DScene& S, int pi, V3 p) {
         const DPrim P = S.prims[pi];
         switch (P.kind) {
@@ -627,6 +751,7 @@ template <int L, int R> struct Obj {
         case PK_SUB:    // a && !b
         case PK_XFORM: {  // child at the inverse-transformed point
             // one call site of the level below (loop not unrolled), as in composite_t
+            if constexpr (!kOneSite) return contains_calls(S, P, p);
             const bool xf = P.kind == PK_XFORM;
             int c0, c1 = -1;
             V3 q = p;

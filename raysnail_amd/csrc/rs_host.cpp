@@ -1235,11 +1235,12 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                     HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
                     ++ki;
                     ++path_launches;
+                    // (the classes' shading kernels on side streams, concurrently after the extend,
+                    // measured slower: bench frame 10.24 -> 10.32 ms)
                     for (int k = 0; k < kWfsClasses; ++k) {
                         if (!(s->class_mask & (1u << k))) continue;  // no prim of this class: empty queue
                         HIP_OK(launch_wfs_shade(ds, WS, R.qptr[k], k, b, cstride, st->depth, pp.n_items, R.d_rad,
-                                                std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, dc, pp, c0,
-                                                stream));
+                                                std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                         ++path_launches;
                     }
                 }
@@ -1317,8 +1318,8 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
     //                 per shaded segment; + throughput record in (32 B), item (4 B) and
     //                 radiance out (24 B) per path ending in extend (sky miss / light hit).
     //                 bounce 0 (fused with ray generation): radiance out (24 B) per sample that
-    //                 ends there (incl. masked); hit (16 B) + queue slot (4 B) per shaded one
-    //                 (the bounce-0 shading kernels regenerate the camera ray, camera_regen)
+    //                 ends there (incl. masked); hit + queue slot + ray records (64 B, rng
+    //                 inside) + throughput record (32 B) + item (4 B) per shaded one
     const uint64_t items = (uint64_t)P.n_pix * P.N;
     uint64_t kbytes;
     if (!P.wavefront) {
@@ -1327,7 +1328,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
     } else if (cstride_f > 1) {
         stats->kernel_id = RS_KERNEL_WFS_EXTEND;
         const uint64_t segr = seg - seg0, contr = cont - cont0;
-        kbytes = 24ull * (items - cont0) + 20ull * cont0 + 64ull * segr + 20ull * contr + 60ull * (segr - contr);
+        kbytes = 24ull * (items - cont0) + 120ull * cont0 + 64ull * segr + 20ull * contr + 60ull * (segr - contr);
     } else {
         stats->kernel_id = RS_KERNEL_WF_EXTEND;
         kbytes = 80ull * seg;

@@ -97,10 +97,9 @@ hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const Path
 uint32_t wfs_extend_batch();
 hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st);
-// bounce 0 regenerates each path from its camera sample (item0 + queued index: c, p, item0)
 hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
-                           const DCamera& c, const PathParams& p, uint64_t item0, hipStream_t st);
+                           hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
 hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
 hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st);

@@ -873,13 +873,6 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
     camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
     return true;
 }
-// The camera ray and stream state of a live item again (the bounce-0 shading kernels recompute them
-// instead of reading a path record that bounce 0 would have had to write: 100 B per path each way)
-__device__ __forceinline__ void camera_regen(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
-    const uint32_t pl = (uint32_t)(item % P.n_pix_local);
-    const uint32_t sl = (uint32_t)(item / P.n_pix_local);
-    camera_sample_xy(C, P, pl % P.width, P.row_begin + (pl / P.width) * P.row_step, P.s0 + sl, r, rng);
-}
 
 __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfState W, uint64_t item0, uint32_t n,
                                                    double* __restrict__ rad) {
@@ -1102,10 +1095,11 @@ __device__ __forceinline__ void ext_sort_batch(const WfSet& cur, uint32_t cap, u
     __syncthreads();
 }
 
-// GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i and traverses it
-// straight from registers; for the paths that go on to shading only the hit (16 B) and the queue slot
-// are written -- the bounce-0 shade kernels regenerate ray and stream state from item0 + i, with
-// T = 1 and L = 0 implied.
+// GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
+// straight from registers, and only the paths that go on to shading are written (at index i, with
+// T = 1 and L = 0 implied for the bounce-0 shade kernels). (Writing only the hit and regenerating the
+// camera ray in the bounce-0 shade kernels instead cut 0.27 GB of HBM traffic per launch but made the
+// bench frame slower, 10.20 -> 10.26 ms: the stores are not what bounds this kernel.)
 #ifndef RS_EXT_MIN_WAVES_SORT
 #define RS_EXT_MIN_WAVES_SORT 4  // spheres, bounces >= 1 (the coherence-sorted batches): 135 -> 127 VGPRs, no spill
 #endif
@@ -1185,8 +1179,9 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
                         }
                         add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
                         cls = -1;
-                    } else {  // bounce 0: the shading kernel regenerates the camera ray (camera_regen)
+                    } else {
                         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+                        if (GEN) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item);
                         done = false;
                     }
                 }
@@ -1245,13 +1240,10 @@ __device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
 #ifndef RS_LAMB_MIN_WAVES
 #define RS_LAMB_MIN_WAVES 4  // 130 -> 128 VGPRs (4 waves/SIMD, 12 B spill): 10.01 -> 9.94 ms bench frame
 #endif
-// FIRST = bounce 0: the path is regenerated from its camera sample (item0 + queued index, see
-// k_wfs_extend<true>) instead of being read from a path record.
-template <int KIND, int SM, bool FIRST>
+template <int KIND, int SM>
 __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest2) ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(const DScene* __restrict__ Sp, WfState W, const uint32_t* __restrict__ queue,
                                                      int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
-                                                     uint64_t n_items, double* __restrict__ rad, DCamera C,
-                                                     PathParams P, uint64_t item0) {
+                                                     uint64_t n_items, double* __restrict__ rad) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
     uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
@@ -1281,18 +1273,12 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
         uint32_t item = 0;
         if (j < n) {
             const uint32_t i = queue[j];
-            if (FIRST) {
-                item = (uint32_t)(item0 + i);
-                camera_regen(C, P, item, r, rng);
-                T = v3(1.0, 1.0, 1.0);
-            } else {
-                load_path(cur, i, r, T, rng);
-                item = cur.item[i];
-            }
+            load_path(cur, i, r, T, rng);
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
             finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
+            item = cur.item[i];
             const int mi = h.mat >= 0 ? h.mat : S.default_mat;
             const DMaterial& M0 = S.mats[mi];
             bool cont;
@@ -1537,13 +1523,13 @@ hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const Path
     return hipGetLastError();
 }
 
-template <int SM, bool FIRST>
+template <int SM>
 static void launch_wfs_shade_sm(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                                 uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks,
-                                const DCamera& c, const PathParams& p, uint64_t item0, hipStream_t st) {
+                                hipStream_t st) {
 #define RS_SHADE_LAUNCH(KIND) \
-    hipLaunchKernelGGL((k_wfs_shade<KIND, SM, FIRST>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, \
-                       stride, depth, n_items, rad, c, p, item0)
+    hipLaunchKernelGGL((k_wfs_shade<KIND, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, \
+                       stride, depth, n_items, rad)
     switch (cls) {
     case 0: RS_SHADE_LAUNCH(RS_MAT_LAMBERTIAN); break;
     case 1: RS_SHADE_LAUNCH(RS_MAT_METAL); break;
@@ -1556,13 +1542,8 @@ static void launch_wfs_shade_sm(const SceneRef& s, const WfState& w, const uint3
 
 hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
-                           const DCamera& c, const PathParams& p, uint64_t item0, hipStream_t st) {
-    if (bounce == 0)
-        RS_SM_SORTED_DISPATCH(sm, (launch_wfs_shade_sm<SMC, true>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks,
-                                                                 c, p, item0, st)));
-    else
-        RS_SM_SORTED_DISPATCH(sm, (launch_wfs_shade_sm<SMC, false>(s, w, queue, cls, bounce, stride, depth, n_items, rad,
-                                                                  blocks, c, p, item0, st)));
+                           hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, launch_wfs_shade_sm<SMC>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st));
     return hipGetLastError();
 }
 

@@ -361,13 +361,40 @@ std::vector<Pixel> TakePhotoSettings::shot_to_target(const char*, World& world, 
     }
     std::vector<Pixel> out(W * H, Pixel{0.f, 0.f, 0.f, 0.f});
     const rs_render_settings st = settings();
-    check_rs(rs_render(world.device_scene(), &cam, &st, mask.empty() ? nullptr : mask.data(),
-                       reinterpret_cast<float*>(out.data()), &stats_));
-    if (target) {
-        for (size_t y = 0; y < H; ++y)
-            target->register_pixels(y, std::vector<Pixel>(out.begin() + y * W, out.begin() + (y + 1) * W));
-        target->register_pixels(H, {});  // end-of-pass sentinel (painter.rs:332)
+    const uint8_t* mp = mask.empty() ? nullptr : mask.data();
+    if (!target) {
+        check_rs(rs_render(world.device_scene(), &cam, &st, mp, reinterpret_cast<float*>(out.data()), &stats_));
+        return out;
     }
+    // Progressive delivery: upstream's workers call register_pixels as each row finishes
+    // (painter.rs:214), which feeds the CLI preview. Here the frame's row lattice is rendered in
+    // kBands bands and each band's rows are handed over as soon as the band is done. Pixels do not
+    // depend on the banding (every sample has its own RNG stream), so the frame is the one-call frame.
+    constexpr uint32_t kBands = 8;
+    const uint32_t rb = st.row_begin, re = st.row_end ? std::min<uint32_t>(st.row_end, (uint32_t)H) : (uint32_t)H;
+    const uint32_t step = st.row_step ? st.row_step : 1;
+    const uint32_t n_rows = rb < re ? (re - rb + step - 1) / step : 0;
+    const uint32_t per = std::max<uint32_t>(1, (n_rows + kBands - 1) / kBands);
+    std::vector<uint8_t> sent(H, 0);
+    stats_ = rs_render_stats{};
+    for (uint32_t r0 = 0; r0 < n_rows; r0 += per) {
+        rs_render_settings bs = st;
+        bs.row_begin = rb + r0 * step;
+        bs.row_end = (uint32_t)std::min<uint64_t>(re, (uint64_t)bs.row_begin + (uint64_t)per * step);
+        bs.row_step = step;
+        rs_render_stats s{};
+        check_rs(rs_render(world.device_scene(), &cam, &bs, mp, reinterpret_cast<float*>(out.data()), &s));
+        stats_.samples += s.samples; stats_.segments += s.segments; stats_.ms += s.ms; stats_.path_ms += s.path_ms;
+        stats_.launches += s.launches; stats_.kernel_launches += s.kernel_launches; stats_.kernel_ms += s.kernel_ms;
+        stats_.kernel_bytes += s.kernel_bytes; stats_.kernel_id = s.kernel_id; stats_.tree_arity = s.tree_arity;
+        for (uint32_t y = bs.row_begin; y < bs.row_end; y += step) {
+            target->register_pixels(y, std::vector<Pixel>(out.begin() + (size_t)y * W, out.begin() + ((size_t)y + 1) * W));
+            sent[y] = 1;
+        }
+    }
+    for (size_t y = 0; y < H; ++y)  // rows off the lattice (untouched: all zero), once each
+        if (!sent[y]) target->register_pixels(y, std::vector<Pixel>(out.begin() + y * W, out.begin() + (y + 1) * W));
+    target->register_pixels(H, {});  // end-of-pass sentinel (painter.rs:332)
     return out;
 }
 

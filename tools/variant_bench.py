@@ -23,7 +23,9 @@ SCENES = {"rtow": ("scenes.rtow_13_1(800, 500)[:2]", 64, 8),
           "quadric": ("scenes.quadric_sdl(512, 512)", 16, 8),
           "mesh": ("scenes.mesh_scene(480, 270, 64, 120)", 16, 8),
           "c4": ("scenes.quadric_sdl(512, 512)", 64, 50),
-          "c5": ("scenes.mesh_scene(960, 540)", 16, 50)}
+          "c5": ("scenes.mesh_scene(960, 540)", 16, 50),
+          "x1": ("scenes.all_feature_scene(400, 400)", 16, 50),
+          "x2": ("scenes.cornell_smoke(300, 300)", 64, 50)}
 
 
 def main():
