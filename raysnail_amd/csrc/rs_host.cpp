@@ -1189,7 +1189,6 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     const uint32_t shade_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.shade_bpc));
     const uint32_t wide = (uint32_t)std::max(1, R.n_cu * 8);
     const uint32_t mega_blocks = wide;
-    const uint32_t ext_batch = wfs_extend_batch();
     ensure_stack_overflow(s, R, (uint64_t)std::max(std::max(ext_blocks, shade_blocks), wide) * kBlock);
     const size_t n_kernel_ev = wavefront ? (size_t)n_chunks_total * st->depth : n_batches;
     P.ev.assign(2 * (size_t)n_batches, nullptr);
@@ -1231,7 +1230,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                                                      std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     else
                         HIP_OK(launch_wfs_extend(ds, WS, R.d_qptrs, b, cstride, pp.n_items, R.d_rad,
-                                                 std::min(wide, (n + ext_batch - 1) / ext_batch), s->scene_mode, stream));
+                                                 std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
                     ++ki;
                     ++path_launches;

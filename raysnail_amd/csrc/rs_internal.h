@@ -93,8 +93,6 @@ constexpr int kCntFront = 6, kCntBack = 7;
 hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
                                 uint32_t blocks, int sm, hipStream_t st);
-// records one block of the bounce >= 1 extend takes per batch (the coherence-sorted batch)
-uint32_t wfs_extend_batch();
 hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,

@@ -1034,77 +1034,18 @@ constexpr int kClsLight = 6;
 #define RS_EXT_MIN_WAVES 1  // 5 forces <=96 VGPRs but spills; measured slower (14.5 vs 13.8 ms)
 #endif
 #ifndef RS_EXT_MIN_WAVES_N2
-#define RS_EXT_MIN_WAVES_N2 1  // nest-2 scenes (CSG of transforms: C4); 3 spills: 56 -> 79 ms on quadric.sdl
+#define RS_EXT_MIN_WAVES_N2 1  // nest-2 scenes (CSG of transforms: C4): 2 waves (bounce 0: 20 B spill) measured equal, 3 waves spills 288 B (C4 48.7 -> 50.4 ms)
 #endif
 #ifndef RS_EXT_MIN_WAVES_N0
 #define RS_EXT_MIN_WAVES_N0 4  // nest-0 scenes (boxes, quadrics: C2): 129 -> 128 VGPRs, example.sdl 10.8 -> 10.3 ms
 #endif
-// Coherence sort of one extend batch (bounces >= 1): records bb .. bb + nb of the path set are
-// counted into direction cells (ext_sort_key) in LDS and s_perm receives their set indices in cell
-// order, so each wave traces rays of one cell (the wave runs the union of its lanes' traversal loops).
-// Pure scheduling: every record is traced once, by a lane of this block, with the same arithmetic.
-#ifndef RS_EXT_SORT_KEY
-#define RS_EXT_SORT_KEY 0  // 0: no sort, 1: direction octant, 2: octant x dominant axis
-#endif
-#ifndef RS_EXT_SORT_R
-#define RS_EXT_SORT_R 4    // records per thread per batch (a batch of R * kBlock is sorted)
-#endif
-constexpr uint32_t kSortCells = 64;
-__device__ __forceinline__ uint32_t ext_sort_key(const D4& d) {
-    const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
-#if RS_EXT_SORT_KEY >= 2
-    const double ax = fabs(d.x), ay = fabs(d.y), az = fabs(d.z);
-    const uint32_t major = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
-    return oct * 3u + major;
-#else
-    return oct;
-#endif
-}
-template <uint32_t R>
-__device__ __forceinline__ void ext_sort_batch(const WfSet& cur, uint32_t cap, uint32_t nf, uint32_t bb, uint32_t nb,
-                                               uint32_t* s_perm) {
-    __shared__ uint32_t s_hist[kSortCells];
-    if (threadIdx.x < kSortCells) s_hist[threadIdx.x] = 0u;
-    __syncthreads();
-    uint32_t ri[R], rk[R], rn[R];
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-        const uint32_t jj = r * kBlock + threadIdx.x;
-        if (jj < nb) {
-            const uint32_t j = bb + jj;
-            ri[r] = j < nf ? j : cap - 1u - (j - nf);
-            rk[r] = ext_sort_key(cur.ray_d[ri[r]]);
-            rn[r] = atomicAdd(&s_hist[rk[r]], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the cell counts (one wave)
-        const uint32_t lane = threadIdx.x, v = lane < kSortCells ? s_hist[lane] : 0u;
-        uint32_t x = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t t = __shfl_up(x, off, 64);
-            if (lane >= (uint32_t)off) x += t;
-        }
-        if (lane < kSortCells) s_hist[lane] = x - v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r)
-        if (r * kBlock + threadIdx.x < nb) s_perm[s_hist[rk[r]] + rn[r]] = ri[r];
-    __syncthreads();
-}
-
 // GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
 // straight from registers, and only the paths that go on to shading are written (at index i, with
 // T = 1 and L = 0 implied for the bounce-0 shade kernels). (Writing only the hit and regenerating the
 // camera ray in the bounce-0 shade kernels instead cut 0.27 GB of HBM traffic per launch but made the
 // bench frame slower, 10.20 -> 10.26 ms: the stores are not what bounds this kernel.)
-#ifndef RS_EXT_MIN_WAVES_SORT
-#define RS_EXT_MIN_WAVES_SORT 4  // spheres, bounces >= 1 (the coherence-sorted batches): 135 -> 127 VGPRs, no spill
-#endif
 template <bool GEN, int SM>
-__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : GEN ? RS_EXT_MIN_WAVES : RS_EXT_MIN_WAVES_SORT) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
+__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
@@ -1116,26 +1057,13 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
     const uint32_t n = GEN ? n_gen : nf + cnt[kCntBack];
     if (!GEN && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n;  // live paths at this bounce (stats)
     const WfSet& cur = W.set[bounce & 1];
-    // bounces >= 1 with a coherence sort: a block takes R * kBlock records per batch and traces them
-    // in direction-cell order (ext_sort_batch), R rounds of kBlock; otherwise one record per thread
-    constexpr bool kSort = !GEN && RS_EXT_SORT_KEY > 0;
-    constexpr uint32_t R = kSort ? RS_EXT_SORT_R : 1u;
-    constexpr uint32_t kBatch = kBlock * R;
-    __shared__ uint32_t s_perm[kSort ? kBatch : 1];
-    for (uint32_t bb = blockIdx.x * kBatch; bb < n; bb += gridDim.x * kBatch) {
-      const uint32_t nb = min(kBatch, n - bb);
-      if constexpr (kSort) ext_sort_batch<R>(cur, W.cap, nf, bb, nb, s_perm);
-      for (uint32_t rr = 0; rr < R; ++rr) {
-        const uint32_t jj = rr * kBlock + threadIdx.x;
-        const bool valid = jj < nb;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
         // thread -> record: the front run [0, nf), then the back run from the set's end down
-        const uint32_t j = bb + jj;
-        uint32_t i;
-        if constexpr (kSort) i = valid ? s_perm[jj] : 0u;
-        else i = (GEN || j < nf) ? j : W.cap - 1u - (j - nf);
+        const uint32_t j = base + threadIdx.x;
+        const uint32_t i = (GEN || j < nf) ? j : W.cap - 1u - (j - nf);
         int cls = -1;
         bool live = false;
-        if (valid) {
+        if (j < n) {
             Ray r;
             Rng rng;
             uint32_t item = 0;
@@ -1205,7 +1133,6 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
         uint32_t* const cs[kClasses] = {&cnt[1], &cnt[2], &cnt[3], &cnt[4], &cnt[5]};
         const uint32_t slot = block_slot<kClasses>(cls, cs);
         if (cls >= 0) queues[cls][slot] = i;
-      }
     }
 }
 
@@ -1504,8 +1431,6 @@ hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce,
     RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_shade<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, depth, n_items, rad));
     return hipGetLastError();
 }
-
-uint32_t wfs_extend_batch() { return RS_EXT_SORT_KEY > 0 ? kBlock * RS_EXT_SORT_R : kBlock; }
 
 hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st) {
