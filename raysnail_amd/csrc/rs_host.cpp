@@ -1187,7 +1187,19 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     // launch grids: grid-stride kernels over at most these many blocks
     const uint32_t ext_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.ext_bpc));
     const uint32_t shade_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.shade_bpc));
-    const uint32_t wide = (uint32_t)std::max(1, R.n_cu * 8);
+#ifndef RS_WIDE_BPC
+#define RS_WIDE_BPC 64  // shading grids (their queue lengths live on the device): 8 -> 64 per CU, 9.22 -> 9.12 ms
+#endif
+    const uint32_t wide = (uint32_t)std::max(1, R.n_cu * RS_WIDE_BPC);
+    // sorted-path extend grids: one block per 256 paths, so no block loops over batches and the hardware
+    // dispatcher refills a CU as soon as one of its blocks ends (bench frame 9.58 -> 9.22 ms against a
+    // grid-stride loop over 8 blocks per CU). A tree deeper than the LDS stack part spills to an HBM
+    // array strided by the grid's threads: such scenes keep a bounded grid-stride grid.
+    const bool ext_spill = s->stack_need > kStackMax;
+    auto ext_grid = [&](uint32_t n) {
+        const uint32_t b = (n + kBlock - 1) / kBlock;
+        return ext_spill ? std::min(wide, b) : b;
+    };
     const uint32_t mega_blocks = wide;
     ensure_stack_overflow(s, R, (uint64_t)std::max(std::max(ext_blocks, shade_blocks), wide) * kBlock);
     const size_t n_kernel_ev = wavefront ? (size_t)n_chunks_total * st->depth : n_batches;
@@ -1227,10 +1239,10 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                     HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
                     if (b == 0)
                         HIP_OK(launch_wfs_gen_extend(ds, dc, pp, WS, R.d_qptrs, cstride, c0, n, R.d_rad,
-                                                     std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
+                                                     ext_grid(n), s->scene_mode, stream));
                     else
                         HIP_OK(launch_wfs_extend(ds, WS, R.d_qptrs, b, cstride, pp.n_items, R.d_rad,
-                                                 std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
+                                                 ext_grid(n), s->scene_mode, stream));
                     HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
                     ++ki;
                     ++path_launches;
@@ -1304,7 +1316,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
             for (uint32_t b = 0; b < P.depth; ++b) {
                 const uint32_t* q = &P.qc[(c * (P.depth + 1) + b) * cstride_f];
                 uint64_t cb = 0;
-                if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cb += q[1 + k];
+                if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cb += q[(1 + k) * kCntPad];
                 if (b == 0) { seg0 += q[0]; cont0 += cb; }
                 seg += q[0];
                 cont += cb;

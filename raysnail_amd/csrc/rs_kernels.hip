@@ -1095,8 +1095,8 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
     __shared__ int stk_all[kStackMax * kBlock];
     const Stk stk = make_stk(S, stk_all);
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
-    const uint32_t nf = GEN ? 0u : cnt[kCntFront];
-    const uint32_t n = GEN ? n_gen : nf + cnt[kCntBack];
+    const uint32_t nf = GEN ? 0u : cnt[kCntFront * kCntPad];
+    const uint32_t n = GEN ? n_gen : nf + cnt[kCntBack * kCntPad];
     if (!GEN && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n;  // live paths at this bounce (stats)
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -1172,7 +1172,7 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
         trav_stats_flush(live);
 #endif
         if (GEN) block_slot1(live, &cnt[0]);  // segments at bounce 0 (stats)
-        uint32_t* const cs[kClasses] = {&cnt[1], &cnt[2], &cnt[3], &cnt[4], &cnt[5]};
+        uint32_t* const cs[kClasses] = {&cnt[1 * kCntPad], &cnt[2 * kCntPad], &cnt[3 * kCntPad], &cnt[4 * kCntPad], &cnt[5 * kCntPad]};
         const uint32_t slot = block_slot<kClasses>(cls, cs);
         if (cls >= 0) queues[cls][slot] = i;
     }
@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
     uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
-    const uint32_t n = cnt[1 + cls];
+    const uint32_t n = cnt[(1 + cls) * kCntPad];
     const WfSet& cur = W.set[bounce & 1];
     const WfSet& nxt = W.set[(bounce + 1) & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -1269,7 +1269,7 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
         }
         // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
         // the front, the rest from the back: the next extend's waves then trace rays of one kind
-        uint32_t* const gc[2] = {&cnt_next[kCntBack], &cnt_next[kCntFront]};
+        uint32_t* const gc[2] = {&cnt_next[kCntBack * kCntPad], &cnt_next[kCntFront * kCntPad]};
         const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
         if (alive) store_path(nxt, light_ray ? slot : W.cap - 1u - slot, r, T, rng, item);
     }
