@@ -1049,13 +1049,14 @@ void ensure_stack_overflow(const rs_scene* s, Replica& R, uint64_t threads) {
 
 WfState carve_wf(Replica& R, uint64_t cap) {
     const size_t per_set = 3 * sizeof(D4) + sizeof(uint32_t);
-    const size_t per = 2 * per_set + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
+    const size_t per = 2 * per_set + sizeof(double2);
+    const uint64_t qcap = (uint64_t)kQSub * qsub_cap((uint32_t)std::max<uint64_t>(cap, R.wf_cap));  // per class queue
     const bool fresh = cap > R.wf_cap;
     if (fresh) {
         if (R.d_wf) HIP_OK(hipFree(R.d_wf));
         R.d_wf = nullptr;
         R.wf_cap = 0;
-        HIP_OK(hipMalloc(&R.d_wf, per * cap + 8192));
+        HIP_OK(hipMalloc(&R.d_wf, per * cap + kWfsClasses * sizeof(uint32_t) * qcap + 8192));
         R.wf_cap = cap;
     }
     char* p = (char*)R.d_wf;
@@ -1071,13 +1072,14 @@ WfState carve_wf(Replica& R, uint64_t cap) {
     }
     w.hit = (double2*)p; p += sizeof(double2) * c;
     uint32_t* qp[kWfsClasses];
-    for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p += sizeof(uint32_t) * c; }
+    for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p += sizeof(uint32_t) * qcap; }
     p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
     R.d_qptrs = (uint32_t**)p;
     if (fresh) HIP_OK(hipMemcpy(R.d_qptrs, qp, sizeof(qp), hipMemcpyHostToDevice));
     for (int k = 0; k < kWfsClasses; ++k) R.qptr[k] = qp[k];
     w.counts = nullptr;
     w.cap = (uint32_t)c;
+    w.qsub = qsub_cap((uint32_t)c);
     return w;
 }
 
@@ -1195,6 +1197,9 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     // dispatcher refills a CU as soon as one of its blocks ends (bench frame 9.58 -> 9.22 ms against a
     // grid-stride loop over 8 blocks per CU). A tree deeper than the LDS stack part spills to an HBM
     // array strided by the grid's threads: such scenes keep a bounded grid-stride grid.
+#ifndef RS_WF_FULL
+#define RS_WF_FULL 0
+#endif
     const bool ext_spill = s->stack_need > kStackMax;
     auto ext_grid = [&](uint32_t n) {
         const uint32_t b = (n + kBlock - 1) / kBlock;
@@ -1257,11 +1262,13 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
                     HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
-                    HIP_OK(launch_wf_extend(ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
+                    HIP_OK(launch_wf_extend(ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock),
+                                            RS_WF_FULL ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
+                                            s->scene_mode, stream));
                     HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
                     ++ki;
                     HIP_OK(launch_wf_shade(ds, WS, b, st->depth, pp.n_items, R.d_rad,
-                                           std::min(shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
+                                           std::min(RS_WF_FULL ? wide : shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     path_launches += 2;
                 }
             }
@@ -1316,7 +1323,9 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
             for (uint32_t b = 0; b < P.depth; ++b) {
                 const uint32_t* q = &P.qc[(c * (P.depth + 1) + b) * cstride_f];
                 uint64_t cb = 0;
-                if (cstride_f > 1) for (int k = 0; k < kWfsClasses; ++k) cb += q[(1 + k) * kCntPad];
+                if (cstride_f > 1)
+                    for (int k = 0; k < kWfsClasses; ++k)
+                        for (uint32_t g = 0; g < kQSub; ++g) cb += q[cix(1 + k, g)];
                 if (b == 0) { seg0 += q[0]; cont0 += cb; }
                 seg += q[0];
                 cont += cb;

@@ -64,6 +64,7 @@ struct WfState {
     double2* hit;         // per compacted slot of the current bounce: (prim as bits, accepted range end)
     uint32_t* counts;     // [depth + 1] live paths per bounce
     uint32_t cap;         // records per set (the sorted path fills a set from both ends, see k_wfs_shade)
+    uint32_t qsub;        // records per class sub-queue (qsub_cap(cap))
 };
 
 struct FinalParams {
@@ -81,7 +82,8 @@ hipError_t launch_path_mega(const SceneRef& s, const DCamera& c, const PathParam
                             unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st);
 hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
                          hipStream_t st);
-hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);
+hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, uint32_t blocks_lockstep,
+                            int sm, hipStream_t st);
 hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st);
 // material-sorted variant (every scene mode but the generic / rich one): counts stride per bounce = kWfsStride
@@ -91,7 +93,20 @@ constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric,
                        // different classes do not serialise on one L2 line (bench frame 9.89 -> 9.58 ms)
 #endif
 constexpr uint32_t kCntPad = RS_CNT_PAD;
-constexpr uint32_t kWfsStride = 8 * kCntPad;
+// Each class queue is split into kQSub sub-queues with a counter each: batch q of 256 paths of an
+// extend launch appends to sub-queue q % kQSub, so the block-aggregated atomics spread over kQSub
+// lines per class instead of serialising on one. A sub-queue holds at most WfState::qsub records
+// (the batches q == g mod kQSub of a set), the shading kernels walk the sub-queues in order.
+#ifndef RS_QSUB
+#define RS_QSUB 1  // measured: 4, 8, 16 sub-queues are slower (bench frame 9.06 -> 9.18, 9.25, 9.39 ms)
+#endif
+constexpr uint32_t kQSub = RS_QSUB;
+constexpr uint32_t kWfsStride = 8 * kQSub * kCntPad;
+// word index of counter `slot` (0 live, 1 + k class k, kCntFront, kCntBack), sub-counter g, in a bounce's block
+__host__ __device__ constexpr uint32_t cix(int slot, uint32_t g = 0) { return ((uint32_t)slot * kQSub + g) * kCntPad; }
+__host__ __device__ constexpr uint32_t qsub_cap(uint32_t cap) {
+    return ((cap + 255u) / 256u + kQSub - 1u) / kQSub * 256u;
+}
 // counts[6] / counts[7] of a bounce: paths written from the front / the back of the set (light-
 // sample rays / the rest), so the next extend's waves hold rays of one kind (k_wfs_shade)
 constexpr int kCntFront = 6, kCntBack = 7;

@@ -819,9 +819,11 @@ __device__ __forceinline__ uint32_t wave_slot(bool flag, uint32_t* counter) {
 // Block-aggregated slot allocation for up to C independent counters: ONE returning atomic per
 // block and counter (a single hot word sustains only ~88 atomics/us, MI355X_MICROARCH.md
 // 'dequeue'), lanes get slots ordered by (wave, lane). Must be called by every thread of the block.
+// With stat != nullptr the block's count of `flag` lanes is also added to *stat (no returned value).
 template <int C>
-__device__ __forceinline__ uint32_t block_slot(int cls, uint32_t* const* counters) {
-    __shared__ uint32_t wcnt[C][kBlock / 64];
+__device__ __forceinline__ uint32_t block_slot(int cls, uint32_t* const* counters, bool flag = false,
+                                               uint32_t* stat = nullptr) {
+    __shared__ uint32_t wcnt[C + 1][kBlock / 64];
     __shared__ uint32_t bbase[C];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long mine = 0ull;
@@ -831,12 +833,20 @@ __device__ __forceinline__ uint32_t block_slot(int cls, uint32_t* const* counter
         if (cls == k) mine = m;
         if (lane == 0) wcnt[k][wave] = (uint32_t)__popcll(m);
     }
+    if (stat) {
+        const unsigned long long m = __ballot(flag);
+        if (lane == 0) wcnt[C][wave] = (uint32_t)__popcll(m);
+    }
     __syncthreads();
     if (threadIdx.x < C) {
         const int k = threadIdx.x;
         uint32_t tot = 0;
         for (int w = 0; w < kBlock / 64; ++w) { const uint32_t c = wcnt[k][w]; wcnt[k][w] = tot; tot += c; }
         bbase[k] = tot ? atomicAdd(counters[k], tot) : 0u;
+    } else if (stat && threadIdx.x == 64) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[C][w];
+        if (tot) atomicAdd(stat, tot);
     }
     __syncthreads();
     uint32_t slot = 0;
@@ -1095,8 +1105,8 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
     __shared__ int stk_all[kStackMax * kBlock];
     const Stk stk = make_stk(S, stk_all);
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
-    const uint32_t nf = GEN ? 0u : cnt[kCntFront * kCntPad];
-    const uint32_t n = GEN ? n_gen : nf + cnt[kCntBack * kCntPad];
+    const uint32_t nf = GEN ? 0u : cnt[cix(kCntFront)];
+    const uint32_t n = GEN ? n_gen : nf + cnt[cix(kCntBack)];
     if (!GEN && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n;  // live paths at this bounce (stats)
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -1171,10 +1181,12 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
 #ifdef RS_TRAV_STATS
         trav_stats_flush(live);
 #endif
-        if (GEN) block_slot1(live, &cnt[0]);  // segments at bounce 0 (stats)
-        uint32_t* const cs[kClasses] = {&cnt[1 * kCntPad], &cnt[2 * kCntPad], &cnt[3 * kCntPad], &cnt[4 * kCntPad], &cnt[5 * kCntPad]};
-        const uint32_t slot = block_slot<kClasses>(cls, cs);
-        if (cls >= 0) queues[cls][slot] = i;
+        // sub-queue of this batch of 256 paths (bounded by WfState::qsub, rs_internal.h)
+        const uint32_t g = (base / kBlock) % kQSub;
+        uint32_t* const cs[kClasses] = {&cnt[cix(1, g)], &cnt[cix(2, g)], &cnt[cix(3, g)], &cnt[cix(4, g)], &cnt[cix(5, g)]};
+        // bounce 0 also counts its live camera samples (segments, stats) in the same block reduction
+        const uint32_t slot = block_slot<kClasses>(cls, cs, live, GEN ? &cnt[cix(0)] : nullptr);
+        if (cls >= 0) queues[cls][g * W.qsub + slot] = i;
     }
 }
 
@@ -1216,7 +1228,11 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
     uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
-    const uint32_t n = cnt[(1 + cls) * kCntPad];
+    // the class queue is kQSub sub-queues: thread j takes entry j of their concatenation
+    uint32_t qn[kQSub];
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < kQSub; ++g) { qn[g] = cnt[cix(1 + cls, g)]; n += qn[g]; }
     const WfSet& cur = W.set[bounce & 1];
     const WfSet& nxt = W.set[(bounce + 1) & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -1241,7 +1257,11 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
         Rng rng;
         uint32_t item = 0;
         if (j < n) {
-            const uint32_t i = queue[j];
+            uint32_t g = 0, off = j;
+#pragma unroll
+            for (uint32_t k = 0; k + 1 < kQSub; ++k)
+                if (g == k && off >= qn[k]) { off -= qn[k]; g = k + 1; }
+            const uint32_t i = queue[g * W.qsub + off];
             load_path(cur, i, r, T, rng);
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
@@ -1269,7 +1289,7 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
         }
         // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
         // the front, the rest from the back: the next extend's waves then trace rays of one kind
-        uint32_t* const gc[2] = {&cnt_next[kCntBack * kCntPad], &cnt_next[kCntFront * kCntPad]};
+        uint32_t* const gc[2] = {&cnt_next[cix(kCntBack)], &cnt_next[cix(kCntFront)]};
         const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
         if (alive) store_path(nxt, light_ray ? slot : W.cap - 1u - slot, r, T, rng, item);
     }
@@ -1459,12 +1479,14 @@ hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w
     return hipGetLastError();
 }
 
-hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st) {
+// blocks: the resident grid (persistent lanes); blocks_lockstep: the grid of the lock-step kernel
+hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, uint32_t blocks_lockstep,
+                            int sm, hipStream_t st) {
     if (sm == kSmFlat && s.host->root4 >= 0 && !getenv_flag_no_pl()) {
         hipLaunchKernelGGL(k_wf_extend_pl<kSmFlat>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce);
         return hipGetLastError();
     }
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce));
+    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks_lockstep), dim3(kBlock), 0, st, s.dev, w, bounce));
     return hipGetLastError();
 }
 
