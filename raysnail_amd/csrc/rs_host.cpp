@@ -1178,7 +1178,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     // are traversal-bound and run faster on the plain wavefront, whose extend kernel is lighter
     // (mesh 480x270x16: 5.8 vs 7.2 ms; example.sdl 8.8 -> 7.6 ms, quadric.sdl 9.9 -> 8.9 ms sorted)
     const bool sorted = wavefront && (s->scene_mode == kSmSpheres || s->scene_mode == kSmNest0 ||
-                                      s->scene_mode == kSmNest2);
+                                      s->scene_mode == kSmNest2 || (RS_SORTED_FLAT && s->scene_mode == kSmFlat));
     const uint32_t cstride = sorted ? kWfsStride : 1;
     if (wavefront && N > 0) {
         WS = carve_wf(R, chunk);
@@ -1198,9 +1198,10 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     // grid-stride loop over 8 blocks per CU). A tree deeper than the LDS stack part spills to an HBM
     // array strided by the grid's threads: such scenes keep a bounded grid-stride grid.
 #ifndef RS_WF_FULL
-#define RS_WF_FULL 0
+#define RS_WF_FULL 1  // meshes: lock-step extend one block per 256 paths, shading 64 blocks/CU (C5 49.6 -> 48.1 ms)
 #endif
     const bool ext_spill = s->stack_need > kStackMax;
+    const bool wf_full = RS_WF_FULL && s->scene_mode == kSmFlat;  // lock-step unsorted grids (meshes only)
     auto ext_grid = [&](uint32_t n) {
         const uint32_t b = (n + kBlock - 1) / kBlock;
         return ext_spill ? std::min(wide, b) : b;
@@ -1263,12 +1264,12 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
                     HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
                     HIP_OK(launch_wf_extend(ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock),
-                                            RS_WF_FULL ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
+                                            wf_full ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
                                             s->scene_mode, stream));
                     HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
                     ++ki;
                     HIP_OK(launch_wf_shade(ds, WS, b, st->depth, pp.n_items, R.d_rad,
-                                           std::min(RS_WF_FULL ? wide : shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
+                                           std::min(wf_full ? wide : shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
                     path_launches += 2;
                 }
             }

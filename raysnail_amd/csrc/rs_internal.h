@@ -87,6 +87,9 @@ hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce
 hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st);
 // material-sorted variant (every scene mode but the generic / rich one): counts stride per bounce = kWfsStride
+#ifndef RS_SORTED_FLAT
+#define RS_SORTED_FLAT 0  // flat scenes (meshes) on the material-sorted wavefront too
+#endif
 constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric, other
 #ifndef RS_CNT_PAD
 #define RS_CNT_PAD 32  // queue counters 128 B apart: one line each, so the block-aggregated atomics of

@@ -14,11 +14,17 @@
 #include "rs_internal.h"
 
 // the material-sorted wavefront's scene modes (rs_host.cpp: spheres, nest-0, nest-2)
+#if RS_SORTED_FLAT
+#define RS_SORTED_FLAT_CASE(...) case kSmFlat: { constexpr int SMC = kSmFlat; __VA_ARGS__; break; }
+#else
+#define RS_SORTED_FLAT_CASE(...)
+#endif
 #define RS_SM_SORTED_DISPATCH(sm, ...)                                     \
     do {                                                                   \
         switch (sm) {                                                      \
         case kSmNest0: { constexpr int SMC = kSmNest0; __VA_ARGS__; break; }     \
         case kSmNest2: { constexpr int SMC = kSmNest2; __VA_ARGS__; break; }     \
+        RS_SORTED_FLAT_CASE(__VA_ARGS__)                                   \
         default: { constexpr int SMC = kSmSpheres; __VA_ARGS__; break; }         \
         }                                                                  \
     } while (0)
