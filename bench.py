@@ -64,7 +64,8 @@ def cpu_baseline(cam, world, spp, depth, seed, row_step, threads):
     _, stats = sc.render(cam.desc, st, threads=threads)
     dt = time.perf_counter() - t0
     n, model, quota = host_cpus()
-    return {"value": stats.samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+    cores = min(threads, n, int(quota) if quota else n)  # CPUs the threads can actually occupy at once
+    return {"value": stats.samples / dt / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
             "threads": threads, "nproc": n, "cpu_model": model, "cgroup_cpu_quota": quota,
             "sample": f"rows 0::{row_step} of the frame ({stats.samples} samples, {stats.segments} segments) "
                       f"in {dt:.1f} s, {threads} threads (num_cpus {n} + 1, painter.rs:321-325) on {model}"
@@ -100,6 +101,9 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-row-step", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = num_cpus + 1 like Painter::draw")
+    ap.add_argument("--row-share", type=int, default=8,
+                    help="at N = 1 also time rows 0::K of the frame (one rank's share at N = K) and report "
+                         "the predicted strong-scaling efficiency T(full) / (K * T(share)); 0 = off")
     args = ap.parse_args()
 
     import torch
@@ -165,6 +169,27 @@ def main():
     dt = float(t.item())
     all_samples, all_segs = float(tot[0].item()), float(tot[1].item())
 
+    share = None
+    if world == 1 and args.row_share > 1:
+        # one rank's work at N = K: the row lattice 0::K of the same frame (render_sharded's split)
+        K = args.row_share
+        for _ in range(args.warmup):
+            render(0, 0, K, 0)
+        torch.cuda.synchronize()
+        sh_launch_ms = 0.0
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            render(0, 0, K, 0)
+            sh_launch_ms += last["stats"].kernel_ms
+        torch.cuda.synchronize()
+        sh_ms = (time.perf_counter() - t1) / args.steps * 1e3
+        full_ms = dt / args.steps * 1e3
+        share = {"K": K, "rows": f"0::{K}", "ms_per_share": round(sh_ms, 4), "ms_full_frame": round(full_ms, 4),
+                 "predicted_efficiency": round(full_ms / (K * sh_ms), 4),
+                 "predicted_speedup": round(full_ms / sh_ms, 3),
+                 "extend_ms_per_share": round(sh_launch_ms / args.steps, 4),
+                 "samples_per_share": int(last["stats"].samples), "launches_per_share": int(last["stats"].launches)}
+
     if rank == 0:
         n_eff = int(args.spp ** 0.5) ** 2
         value = all_samples / dt / 1e6
@@ -182,6 +207,12 @@ def main():
                 "alg_bytes_per_launch": int(bytes_per_launch), "launches_per_step": kern_launches // args.steps,
                 "kernel_share_of_step": round(kern_ms / args.steps / (dt / args.steps * 1e3), 4),
                 "segments_per_sample": round(segs / max(1, samples), 4)}
+        # SURVEY 8(d)'s fixed fp32 model for the same kernel: extend reads a 28 B ray and writes a 16 B
+        # hit per segment (44 B); the builder's f64 byte model above is the `frac` field
+        seg_per_launch = segs / max(1, kern_launches)
+        if avg_launch_s > 0:
+            roof["achieved_s8d"] = round(44.0 * seg_per_launch / avg_launch_s / 1e9, 2)
+            roof["frac_s8d"] = round(roof["achieved_s8d"] / HBM_PEAK_GBS, 5)
         cpu = None
         if args.cpu_baseline and world == 1:
             log("timing CPU baseline (oracle restatement) ...")
@@ -199,6 +230,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if share:
+            line["row_share"] = share
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)

@@ -63,6 +63,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
                                 C.POINTER(C.c_double)]
     lib.orc_scatter.restype = C.c_int
     lib.orc_set_trace.argtypes = [C.c_int]
+    lib.orc_set_variant.argtypes = [C.c_int]
+    lib.orc_set_axis_bits.argtypes = [C.c_uint64]
     lib.orc_chacha_block.argtypes = [C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_uint32)]
     lib.orc_rtow_balls.argtypes = [C.c_uint64, C.POINTER(C.c_double), C.c_int]
     lib.orc_rtow_balls.restype = C.c_int
@@ -70,6 +72,33 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib.orc_rtow_scene.restype = C.c_int
     _LIBS[path] = lib
     return lib
+
+
+# Diagnostic semantics switches (oracle.cpp ORC_VAR_*): hypotheses about the code version behind the
+# reference's own render. Every parity test runs with 0 (the checkout's semantics).
+VAR_LIGHT_RADIUS = 1
+VAR_LIGHT_FROM_POINT = 2
+VAR_SORTED_ROOTS = 4
+VAR_REF_TREE = 8
+VAR_RECT_CLOSED_END = 16
+VAR_TREE_FILE_ORDER = 32
+
+
+class variant:
+    """with variant(VAR_...): scenes committed and rendered inside use that semantics."""
+
+    def __init__(self, bits: int, axis_bits: int = 0, path: str = LIB_PATH):
+        self.lib, self.bits, self.axis_bits = load(path), bits, axis_bits
+
+    def __enter__(self):
+        self.lib.orc_set_variant(self.bits)
+        self.lib.orc_set_axis_bits(self.axis_bits)
+        return self
+
+    def __exit__(self, *exc):
+        self.lib.orc_set_variant(0)
+        self.lib.orc_set_axis_bits(0)
+        return False
 
 
 class OracleScene:

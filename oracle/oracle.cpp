@@ -75,6 +75,18 @@
 namespace orc {
 
 static const double PI = 3.14159265358979323846;
+// Diagnostics only (orc_set_variant; tools/pin_variants.py, tests/test_reference_render_pin.py):
+// hypotheses about the code version that produced the reference's own render
+// (examples/sdl_quadrics.jpg). 0 = the checkout's semantics, which every parity test uses.
+enum {
+    ORC_VAR_LIGHT_RADIUS = 1,        // Sphere::random offsets scaled by the radius (sphere.rs:149-164 ignores it)
+    ORC_VAR_LIGHT_FROM_POINT = 2,    // light-sample ray from hit.point, not ray.at(t1 - 2e-4) (camera.rs:211)
+    ORC_VAR_SORTED_ROOTS = 4,        // Quadric roots tried smaller first (quadric.rs:167-177 tries (-b-sqrt d)/a first)
+    ORC_VAR_REF_TREE = 8,            // bvh.rs:58-113's tree: Random::range(0..2) axes (orc_set_axis_bits), 2-object leaves
+    ORC_VAR_RECT_CLOSED_END = 16,    // AARect::hit accepts t == range end (rect.rs:102 uses the half-open Range)
+    ORC_VAR_TREE_FILE_ORDER = 32,    // BVH over the objects in file order (no sort by bbox min)
+};
+static int g_variant = 0;
 
 // ---------------------------------------------------------------- Vec3 (vec3.rs) ----
 struct Vec3 {
@@ -783,7 +795,7 @@ struct Sphere : Hittable {  // sphere.rs
             Vec3 u = uvw.axis[0] * rng.gen();
             Vec3 v = uvw.axis[1] * rng.gen();
             Vec3 uvv = u + v;
-            if (uvv.length_squared() < 1.0) return (uvv + center) - origin;
+            if (uvv.length_squared() < 1.0) return ((g_variant & ORC_VAR_LIGHT_RADIUS) ? uvv * radius + center : uvv + center) - origin;
         }
         return center - origin;
     }
@@ -804,7 +816,7 @@ struct AARect : Hittable {  // rect.rs
     void uv(const Vec3& p, double& u, double& v) const override { u = (p[ax0] - a0) / a_len; v = (p[ax1] - b0) / b_len; }
     bool hit(const Ray& ray, double tmin, double tmax, HitRecord& rec) const override {  // rect.rs:101-120
         double t1 = (k - ray.origin[ax2]) / ray.direction[ax2];
-        if (!range_contains(t1, tmin, tmax)) return false;
+        if (!range_contains(t1, tmin, tmax) && !((g_variant & ORC_VAR_RECT_CLOSED_END) && t1 == tmax)) return false;
         double a = std::fma(t1, ray.direction[ax0], ray.origin[ax0]);
         if (a < a0 || a > a1) return false;
         double b = std::fma(t1, ray.direction[ax1], ray.origin[ax1]);
@@ -901,6 +913,7 @@ struct Quadric : Hittable {  // quadric.rs
             double dr = std::sqrt(d);
             double t1 = (-b - dr) / a;
             double t2 = (-b + dr) / a;
+            if ((g_variant & ORC_VAR_SORTED_ROOTS) && t2 < t1) std::swap(t1, t2);
             if (range_contains(t1, tmin, tmax)) { rec = make_hit(ray, *this, t1, t2); return true; }
             if (range_contains(t2, tmin, tmax)) { rec = make_hit(ray, *this, t2, 1.7976931348623157e308); return true; }
         }
@@ -1081,7 +1094,10 @@ struct BVHNode {
     AABB box;
     int left = -1, right = -1;  // child node indices
     const Hittable* obj = nullptr;  // leaf
+    bool nobox = false;             // a member of a 2-object leaf (bvh.rs:74-88): no own box test
 };
+static uint64_t g_axis_bits = 0;    // diagnostics (ORC_VAR_REF_TREE): bvh.rs's Random::range(0..2) draws, preorder
+static int g_axis_pos = 0;
 struct BVH {
     std::vector<BVHNode> nodes;
     int root = -1;
@@ -1091,6 +1107,7 @@ struct BVH {
         std::vector<std::pair<const Hittable*, std::pair<AABB, AABB>>> items;  // (obj, (sortbox, box))
         for (auto& o : objs) items.push_back({o.first, {o.first->bbox(0.0, 0.0), o.second}});
         (void)t0; (void)t1;
+        g_axis_pos = 0;
         root = build_rec(items, 0, items.size());
     }
     int build_rec(std::vector<std::pair<const Hittable*, std::pair<AABB, AABB>>>& it, size_t b, size_t e) {
@@ -1101,6 +1118,13 @@ struct BVH {
             nodes[idx].obj = it[b].first;
             return idx;
         }
+        if ((g_variant & ORC_VAR_REF_TREE) && e - b == 2) {
+            int l = build_rec(it, b, b + 1), r = build_rec(it, b + 1, e);
+            nodes[l].nobox = nodes[r].nobox = true;
+            nodes[idx].left = l; nodes[idx].right = r;
+            nodes[idx].box = nodes[l].box | nodes[r].box;
+            return idx;
+        }
         // find_best_axis (bvh.rs:116-169) over the node's objects
         AABB u = it[b].second.second;
         for (size_t i = b + 1; i < e; ++i) u = u | it[i].second.second;
@@ -1109,7 +1133,8 @@ struct BVH {
         if (size.x > size.y && size.x > size.z) axis = 0;
         else if (size.y > size.x && size.y > size.z) axis = 1;
         else if (size.z > size.x && size.z > size.y) axis = 2;
-        std::stable_sort(it.begin() + b, it.begin() + e, [axis](const auto& p, const auto& q) {
+        if (g_variant & ORC_VAR_REF_TREE) axis = (int)((g_axis_bits >> (g_axis_pos++)) & 1);
+        if (!(g_variant & ORC_VAR_TREE_FILE_ORDER)) std::stable_sort(it.begin() + b, it.begin() + e, [axis](const auto& p, const auto& q) {
             return p.second.first.min[axis] < q.second.first.min[axis];
         });
         size_t mid = b + (e - b) / 2;
@@ -1122,7 +1147,7 @@ struct BVH {
     // bvh.rs:173-192
     bool hit(int n, const Ray& ray, double tmin, double tmax, HitRecord& rec) const {
         const BVHNode& node = nodes[n];
-        if (!node.box.hit(ray, tmin, tmax)) return false;
+        if (!node.nobox && !node.box.hit(ray, tmin, tmax)) return false;
         if (node.obj) return node.obj->hit(ray, tmin, tmax, rec);
         HitRecord hl;
         bool okl = hit(node.left, ray, tmin, tmax, hl);
@@ -1254,7 +1279,7 @@ static Vec3 ray_color(const Scene& sc, const Ray& ray, uint32_t depth, FastRng& 
                 Settings st = material->settings();
                 if (st.phong_factor > 0.0)
                     light_multi += phong_highlight(-dir_to_light, ray.direction, hit.normal, st.phong_exponent, st.phong_factor);
-                Vec3 start = ray.at(hit.t1 - 0.0002);
+                Vec3 start = (g_variant & ORC_VAR_LIGHT_FROM_POINT) ? hit.point : ray.at(hit.t1 - 0.0002);
                 scattered = Ray(start, dir_to_light, ray.time);
             } else {
                 Vec3 sd = srec.pdf.generate(rng);
@@ -1288,6 +1313,8 @@ static int fail(int code, const char* msg) { g_err = msg; return code; }
 
 const char* orc_last_error(void) { return g_err.c_str(); }
 void orc_set_trace(int on) { g_trace = on; }
+void orc_set_variant(int v) { g_variant = v; }
+void orc_set_axis_bits(uint64_t b) { g_axis_bits = b; }
 uint64_t orc_stream_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
     return stream_key(seed, pass, pixel, sample);
 }

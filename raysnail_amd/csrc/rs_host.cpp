@@ -855,7 +855,11 @@ void build(rs_scene* s) {
     d.root4 = -1;
     s->tree_arity = root >= 0 ? 2 : 0;
     s->n_nodes = B.nodes.size();
-    if (root >= 0) s->stack_need = s->ref_order ? stack_need_ref(B.nodes, root) : stack_need2(B.nodes, root);
+    // the binary tree is walked in reference order by ref_order scenes and, whatever ref_order says,
+    // by the nest-0 / nest-2 modes (traverse_body), near-first otherwise: size for the larger need
+    if (root >= 0)
+        s->stack_need = s->ref_order ? stack_need_ref(B.nodes, root)
+                                     : std::max(stack_need_ref(B.nodes, root), stack_need2(B.nodes, root));
     if (!s->ref_order && root >= 0 && !std::getenv("RS_NO_BVH4")) {
         std::vector<HNode4> n4;
         int depth4 = 0;
@@ -1385,7 +1389,13 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
     const size_t npx = (size_t)cam->width * cam->height;
     std::vector<std::unique_ptr<Pending>> P(n);
     std::vector<hipEvent_t> done(n, nullptr);
+    hipEvent_t entry = nullptr;  // what the caller queued on `stream` before this call (mask fill, d_out use)
     try {
+        if (n > 1) {
+            DeviceGuard g(s->reps[0]->device);
+            HIP_OK(hipEventCreateWithFlags(&entry, hipEventDisableTiming));
+            HIP_OK(hipEventRecord(entry, stream));
+        }
         for (uint32_t k = 0; k < n; ++k) {
             Replica& R = *s->reps[k];
             P[k].reset(new Pending());
@@ -1396,6 +1406,8 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
                 continue;
             }
             if (rows.count() == 0) continue;
+            // the side streams read d_mask and write d_out: order them after the caller's work
+            HIP_OK(hipStreamWaitEvent(R.stream, entry, 0));
             ensure(R.d_out, R.out_cap, npx * 4);
             const uint8_t* m = nullptr;
             if (d_mask) {
@@ -1423,9 +1435,11 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
         for (uint32_t k = 0; k < n; ++k)  // drain what was enqueued before the buffers go away
             if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipStreamSynchronize(P[k]->stream); }
         for (hipEvent_t e : done) if (e) (void)hipEventDestroy(e);
+        if (entry) (void)hipEventDestroy(entry);
         throw;
     }
     for (hipEvent_t e : done) if (e) (void)hipEventDestroy(e);
+    if (entry) (void)hipEventDestroy(entry);
     acc.tree_arity = s->tree_arity;
     acc.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (stats) *stats = acc;
