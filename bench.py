@@ -127,10 +127,19 @@ def main():
     frame = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     last = {}
 
+    timed = {"on": False}
+    n_eff = int(args.spp ** 0.5) ** 2
+
     def render(rb, re, rs, pass_index):
         st = photo.rows(rb, re, rs).pass_index(pass_index).settings()
-        stats = ds.render_device(cam.desc, st, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        last["stats"] = stats
+        # asynchronous frames (rs_render_device without stats) in the timed region; the kernel
+        # timing / byte statistics come from the same frames rendered with stats (synchronous) below
+        stats = ds.render_device(cam.desc, st, frame.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                 stats=timed["on"])
+        if stats is not None:
+            last["stats"] = stats
+        rows = len(range(rb, re or H, rs))
+        last["samples"] = last.get("samples", 0) + rows * W * n_eff
         return frame
 
     def step():
@@ -142,12 +151,24 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    last["samples"] = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    samples = last["samples"]
+    # the dominant kernel's launches, event-timed (the events ride on the dispatches themselves), and
+    # the library's byte / segment counts: the same K frames again with stats
+    timed["on"] = True
     kern_ms = 0.0
     kern_launches = 0
     kern_bytes = 0
     segs = 0
-    samples = 0
-    t0 = time.perf_counter()
+    stat_samples = 0
     for _ in range(args.steps):
         step()
         st = last["stats"]
@@ -155,12 +176,10 @@ def main():
         kern_launches += st.kernel_launches
         kern_bytes += st.kernel_bytes
         segs += st.segments
-        samples += st.samples
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+        stat_samples += st.samples
+    timed["on"] = False
+    if stat_samples != samples:
+        log(f"warning: stats counted {stat_samples} samples, the timed loop {samples}")
     t = torch.tensor([dt], dtype=torch.float64, device="cuda")
     tot = torch.tensor([float(samples), float(segs)], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -176,13 +195,17 @@ def main():
         for _ in range(args.warmup):
             render(0, 0, K, 0)
         torch.cuda.synchronize()
-        sh_launch_ms = 0.0
         t1 = time.perf_counter()
         for _ in range(args.steps):
             render(0, 0, K, 0)
-            sh_launch_ms += last["stats"].kernel_ms
         torch.cuda.synchronize()
         sh_ms = (time.perf_counter() - t1) / args.steps * 1e3
+        timed["on"] = True
+        sh_launch_ms = 0.0
+        for _ in range(args.steps):
+            render(0, 0, K, 0)
+            sh_launch_ms += last["stats"].kernel_ms
+        timed["on"] = False
         full_ms = dt / args.steps * 1e3
         share = {"K": K, "rows": f"0::{K}", "ms_per_share": round(sh_ms, 4), "ms_full_frame": round(full_ms, 4),
                  "predicted_efficiency": round(full_ms / (K * sh_ms), 4),
@@ -191,7 +214,6 @@ def main():
                  "samples_per_share": int(last["stats"].samples), "launches_per_share": int(last["stats"].launches)}
 
     if rank == 0:
-        n_eff = int(args.spp ** 0.5) ** 2
         value = all_samples / dt / 1e6
         # roofline of the dominant kernel, rank 0's launches: algorithmic bytes per launch (library
         # model from the queue counts, DESIGN.md Roofline) / mean event-timed launch duration

@@ -278,8 +278,12 @@ int rs_scene_get_info(const rs_scene* s, rs_scene_info* out);
 int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st,
               const uint8_t* mask, float* out_rgba, rs_render_stats* stats);
 /* device output: d_out_rgba device pointer (W*H*4 floats), d_mask device pointer or NULL,
- * stream = hipStream_t or NULL (default stream). Returns after the work is enqueued AND
- * complete (the call synchronises its stream) so that stats are final. With several devices
+ * stream = hipStream_t or NULL (default stream). With stats != NULL the call returns after the
+ * work is enqueued AND complete (it synchronises its stream) so that stats are final, and times
+ * the dominant kernel's launches; with stats == NULL it returns once the frame is enqueued
+ * (asynchronous, no timing events): the frame is complete when `stream` reaches this point, and
+ * the next call may be made at once (a call on another stream waits for this frame's buffers).
+ * With several devices
  * (rs_scene_commit_devices) d_out_rgba, d_mask and stream belong to the FIRST listed device, which
  * renders its rows in place; the other devices render on their own streams and copy their rows
  * into d_out_rgba at frame end (peer access where the devices allow it). Stats are summed over

@@ -564,11 +564,14 @@ class DeviceScene:
         return out, stats
 
     def render_device(self, cam: A.rs_camera_desc, st: A.rs_render_settings, d_out_ptr: int,
-                      stream_ptr: int = 0, d_mask_ptr: int = 0) -> A.rs_render_stats:
-        stats = A.rs_render_stats()
+                      stream_ptr: int = 0, d_mask_ptr: int = 0, stats: bool = True):
+        """rs_render_device. stats=True: synchronous, returns rs_render_stats (kernel timing included);
+        stats=False: returns None as soon as the frame is enqueued on the stream (asynchronous)."""
+        out = A.rs_render_stats() if stats else None
         _check(self.lib, self.lib.rs_render_device(self.handle, C.byref(cam), C.byref(st), d_mask_ptr or None,
-                                                   C.c_void_p(d_out_ptr), stream_ptr or None, C.byref(stats)), "rs_")
-        return stats
+                                                   C.c_void_p(d_out_ptr), stream_ptr or None,
+                                                   C.byref(out) if stats else None), "rs_")
+        return out
 
 
 # ----------------------------------------------------------------------------- camera ----

@@ -176,11 +176,29 @@ struct Replica {
     void* d_wf = nullptr; size_t wf_cap = 0;
     uint32_t* d_counts = nullptr; size_t counts_cap = 0;
     int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
-    uint32_t** d_qptrs = nullptr;                 // device array of the per-class queues
-    uint32_t* qptr[kWfsClasses] = {nullptr};
+    // wavefront lanes: independent chunks of a batch in flight together on lane streams (lane 0 =
+    // the caller's stream), each with its own path sets and class queues
+    uint32_t wf_lanes = 0;
+    uint32_t** d_qptrs[kMaxLanes] = {nullptr};    // per lane: device array of the per-class queues
+    uint32_t* qptr[kMaxLanes][kWfsClasses] = {{nullptr}};
+    WfState lane_ws[kMaxLanes]{};
+    hipStream_t lane_stream[kMaxLanes] = {nullptr};  // [1..]: created on first use
+    hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {nullptr};
     int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond kStackMax)
     DScene* d_ds = nullptr;                 // ds in device memory (what the kernels read)
     DScene uploaded{};                      // the copy last written to d_ds
+    // asynchronous frames (rs_render_device without stats): the end of the last enqueued frame, so a
+    // frame on another stream waits for it before reusing the replica's buffers
+    hipEvent_t busy = nullptr;
+    hipStream_t busy_stream = nullptr;
+    // launch-grid sizing: the live paths per bounce of chunk 0 of an earlier frame with the same
+    // workload key, copied back asynchronously (h_hist, hist_ev) and consumed once complete. Any grid
+    // is correct (the kernels loop grid-stride); the prediction only avoids dispatching tens of
+    // thousands of blocks that find no path (they cost ~20 us per late-bounce launch)
+    uint32_t* h_hist = nullptr; size_t hist_cap = 0;
+    hipEvent_t hist_ev = nullptr;
+    uint64_t hist_key = 0, pred_key = 0;
+    std::vector<uint32_t> pred;
 
     // the scene for a launch, with d_ds brought up to date first (it changes only when the
     // stack-overflow array is reallocated)
@@ -195,10 +213,19 @@ struct Replica {
     ~Replica() {
         int prev = -1;
         const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
+        if (busy) (void)hipEventSynchronize(busy);  // an asynchronous frame may still read the scene
         for (void* p : dev) (void)hipFree(p);
         for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts,
                         (void*)d_ovf, (void*)d_ds})
             if (p) (void)hipFree(p);
+        for (uint32_t l = 1; l < kMaxLanes; ++l) {
+            if (lane_stream[l]) (void)hipStreamDestroy(lane_stream[l]);
+            if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
+        }
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (h_hist) (void)hipHostFree(h_hist);
+        if (hist_ev) (void)hipEventDestroy(hist_ev);
+        if (busy) (void)hipEventDestroy(busy);
         if (stream) (void)hipStreamDestroy(stream);
         if (switched) (void)hipSetDevice(prev);
     }
@@ -218,6 +245,7 @@ struct rs_scene {
     HostScene hs;                           // device layout, built once by commit
     std::vector<std::unique_ptr<Replica>> reps;   // the devices the scene is committed to, in call order
     uint64_t wf_chunk = 32ull << 20;              // RS_WF_CHUNK overrides
+    uint32_t wf_lanes = RS_LANES;                 // wavefront lanes (concurrent chunk streams); RS_LANES overrides
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
     uint64_t max_items_per_batch = 32ull << 20;  // RS_MAX_BATCH_ITEMS overrides (tests)
     int tree_depth = 0;                     // levels of the tree in use
@@ -865,6 +893,8 @@ void build(rs_scene* s) {
         int depth4 = 0;
         const int32_t r4 = collapse4(B.nodes, root, n4, 0, depth4);
         if (r4 >= 0) {
+            // the kernels address nodes with 32-bit byte offsets (rs_kernels.hip gld)
+            if (n4.size() * sizeof(DNode4) > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "scene too large: 4-wide tree over 4 GiB");
             std::vector<DNode4> dn4;
             for (const HNode4& h : n4) dn4.push_back(to_device4(h));
             stage(s, d.nodes4, dn4);
@@ -876,6 +906,9 @@ void build(rs_scene* s) {
         }
     }
     d.stack_need = s->stack_need;
+    d.moving = 0;
+    for (const DSphere& sp : spheres)
+        if (sp.v[0] != 0.0 || sp.v[1] != 0.0 || sp.v[2] != 0.0) d.moving = 1;
     d.stk_ovf = nullptr;  // sized per launch grid (ensure_stack_overflow)
     stage(s, d.prims, prims);
     stage(s, d.spheres, spheres);
@@ -1036,7 +1069,7 @@ uint64_t splitmix64_h(uint64_t x) {
 template <typename T>
 void ensure(T*& p, size_t& cap, size_t n) {
     if (n <= cap) return;
-    if (p) HIP_OK(hipFree(p));
+    if (p) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipFree(p)); }  // frames may still be in flight
     p = nullptr;
     HIP_OK(hipMalloc((void**)&p, n * sizeof(T)));
     cap = n;
@@ -1051,40 +1084,45 @@ void ensure_stack_overflow(const rs_scene* s, Replica& R, uint64_t threads) {
     R.ds.stk_ovf = R.d_ovf;
 }
 
-WfState carve_wf(Replica& R, uint64_t cap) {
+// Path state of `lanes` lanes of capacity `cap` paths each (R.lane_ws[l], R.d_qptrs[l], R.qptr[l]).
+void carve_wf(Replica& R, uint64_t cap, uint32_t lanes) {
     const size_t per_set = 3 * sizeof(D4) + sizeof(uint32_t);
     const size_t per = 2 * per_set + sizeof(double2);
-    const uint64_t qcap = (uint64_t)kQSub * qsub_cap((uint32_t)std::max<uint64_t>(cap, R.wf_cap));  // per class queue
-    const bool fresh = cap > R.wf_cap;
+    const uint64_t c = std::max<uint64_t>(cap, R.wf_cap);
+    const uint64_t qcap = (uint64_t)kQSub * qsub_cap((uint32_t)c);  // per class queue
+    const size_t lane_bytes = (per * c + kWfsClasses * sizeof(uint32_t) * qcap + 8192 + 255) & ~(size_t)255;
+    const bool fresh = cap > R.wf_cap || lanes > R.wf_lanes;
     if (fresh) {
-        if (R.d_wf) HIP_OK(hipFree(R.d_wf));
+        if (R.d_wf) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipFree(R.d_wf)); }
         R.d_wf = nullptr;
         R.wf_cap = 0;
-        HIP_OK(hipMalloc(&R.d_wf, per * cap + kWfsClasses * sizeof(uint32_t) * qcap + 8192));
-        R.wf_cap = cap;
+        R.wf_lanes = 0;
+        HIP_OK(hipMalloc(&R.d_wf, lane_bytes * lanes));
+        R.wf_cap = c;
+        R.wf_lanes = lanes;
     }
-    char* p = (char*)R.d_wf;
-    const uint64_t c = R.wf_cap;
-    WfState w;
-    for (int k = 0; k < 2; ++k) {
-        WfSet& t = w.set[k];
-        t.ray_o = (D4*)p; p += sizeof(D4) * c;
-        t.ray_d = (D4*)p; p += sizeof(D4) * c;
-        t.thr = (D4*)p; p += sizeof(D4) * c;
-        t.item = (uint32_t*)p; p += sizeof(uint32_t) * c;
+    for (uint32_t l = 0; l < lanes; ++l) {
+        char* p = (char*)R.d_wf + lane_bytes * l;
+        WfState& w = R.lane_ws[l];
+        for (int k = 0; k < 2; ++k) {
+            WfSet& t = w.set[k];
+            t.ray_o = (D4*)p; p += sizeof(D4) * c;
+            t.ray_d = (D4*)p; p += sizeof(D4) * c;
+            t.thr = (D4*)p; p += sizeof(D4) * c;
+            t.item = (uint32_t*)p; p += sizeof(uint32_t) * c;
+            p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+        }
+        w.hit = (double2*)p; p += sizeof(double2) * c;
+        uint32_t* qp[kWfsClasses];
+        for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p += sizeof(uint32_t) * qcap; }
         p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+        R.d_qptrs[l] = (uint32_t**)p;
+        if (fresh) HIP_OK(hipMemcpy(R.d_qptrs[l], qp, sizeof(qp), hipMemcpyHostToDevice));
+        for (int k = 0; k < kWfsClasses; ++k) R.qptr[l][k] = qp[k];
+        w.counts = nullptr;
+        w.cap = (uint32_t)c;
+        w.qsub = qsub_cap((uint32_t)c);
     }
-    w.hit = (double2*)p; p += sizeof(double2) * c;
-    uint32_t* qp[kWfsClasses];
-    for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p += sizeof(uint32_t) * qcap; }
-    p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
-    R.d_qptrs = (uint32_t**)p;
-    if (fresh) HIP_OK(hipMemcpy(R.d_qptrs, qp, sizeof(qp), hipMemcpyHostToDevice));
-    for (int k = 0; k < kWfsClasses; ++k) R.qptr[k] = qp[k];
-    w.counts = nullptr;
-    w.cap = (uint32_t)c;
-    w.qsub = qsub_cap((uint32_t)c);
-    return w;
 }
 
 struct DeviceGuard {
@@ -1120,7 +1158,7 @@ struct Pending {
     Replica* R = nullptr;
     hipStream_t stream = nullptr;
     bool empty = true;
-    bool wavefront = false, sorted = false;
+    bool wavefront = false, sorted = false, timed = false;
     uint32_t n_pix = 0, N = 0, depth = 0, n_batches = 0, path_launches = 0;
     uint64_t n_chunks_total = 0;
     size_t ki = 0;
@@ -1149,9 +1187,11 @@ void validate_render(const rs_scene* s, const rs_camera_desc* cam, const rs_rend
 // samples -> wavefront or megakernel -> ordered accumulation -> into_color into d_out (W*H RGBA on
 // R's device). Nothing here waits for the device.
 void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, const rs_render_settings* st,
-                    RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t stream, Pending& P) {
+                    RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t stream, Pending& P, bool timed) {
     P.R = &R;
     P.stream = stream;
+    P.timed = timed;
+    if (R.busy && R.busy_stream != stream) HIP_OK(hipStreamWaitEvent(stream, R.busy, 0));
     const bool wavefront = st->mode != RS_MODE_MEGAKERNEL;
     const uint32_t W = cam->width, H = cam->height;
     const uint32_t n_rows = rows.count();
@@ -1174,21 +1214,40 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     if (spb) ensure(R.d_rad, R.rad_cap, (size_t)3 * n_pix * spb);
 
     const uint32_t n_batches = spb ? (N + spb - 1) / spb : 0;
-    const uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(s->wf_chunk, (uint64_t)n_pix * std::max(spb, 1u)));
+    // Wavefront lanes (RS_LANES, default 2): a batch's chunks go round-robin to lane streams and run
+    // concurrently, so one lane's launch tails and small late-bounce launches overlap the other's
+    // work (a strong-scaled share of a frame has many of those). Chunks are whole sample planes when
+    // the batch allows (camera-ray tile order, gen_perm). Scenes whose traversal stack spills to HBM
+    // keep one lane (the overflow array is shared by blockIdx).
+    const bool ext_spill = s->stack_need > kStackMax;
+    uint32_t lanes = (wavefront && N > 0 && !ext_spill) ? std::min<uint32_t>(kMaxLanes, s->wf_lanes) : 1u;
+    uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(s->wf_chunk, (uint64_t)n_pix * std::max(spb, 1u)));
+    if (lanes > 1) {
+        const uint64_t planes = (std::max(spb, 1u) + lanes - 1) / lanes;
+        const uint64_t split = std::max<uint64_t>(kBlock, spb >= lanes ? (uint64_t)n_pix * planes
+                                                                       : ((uint64_t)n_pix * spb + lanes - 1) / lanes);
+        chunk = std::min(chunk, split);
+    }
     uint64_t n_chunks_total = 0;
     for (uint32_t s0 = 0; s0 < N; s0 += spb) n_chunks_total += ((uint64_t)n_pix * std::min(spb, N - s0) + chunk - 1) / chunk;
-    WfState WS{};
+    if (n_chunks_total < lanes) lanes = std::max<uint32_t>(1, (uint32_t)n_chunks_total);
     // material-sorted shading (k_wfs_*) for the spheres / nest-0 / nest-2 modes; flat scenes (meshes)
     // are traversal-bound and run faster on the plain wavefront, whose extend kernel is lighter
     // (mesh 480x270x16: 5.8 vs 7.2 ms; example.sdl 8.8 -> 7.6 ms, quadric.sdl 9.9 -> 8.9 ms sorted)
     const bool sorted = wavefront && (s->scene_mode == kSmSpheres || s->scene_mode == kSmNest0 ||
                                       s->scene_mode == kSmNest2 || (RS_SORTED_FLAT && s->scene_mode == kSmFlat));
     const uint32_t cstride = sorted ? kWfsStride : 1;
+    hipStream_t ls[kMaxLanes] = {stream};
     if (wavefront && N > 0) {
-        WS = carve_wf(R, chunk);
+        carve_wf(R, chunk, lanes);
         const size_t nc = (size_t)n_chunks_total * (st->depth + 1) * cstride;
         ensure(R.d_counts, R.counts_cap, nc);
-        WS.counts = R.d_counts;
+        for (uint32_t l = 1; l < lanes; ++l) {
+            if (!R.lane_stream[l]) HIP_OK(hipStreamCreateWithFlags(&R.lane_stream[l], hipStreamNonBlocking));
+            if (!R.join_ev[l]) HIP_OK(hipEventCreateWithFlags(&R.join_ev[l], hipEventDisableTiming));
+            ls[l] = R.lane_stream[l];
+        }
+        if (lanes > 1 && !R.fork_ev) HIP_OK(hipEventCreateWithFlags(&R.fork_ev, hipEventDisableTiming));
     }
     // launch grids: grid-stride kernels over at most these many blocks
     const uint32_t ext_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.ext_bpc));
@@ -1204,7 +1263,6 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
 #ifndef RS_WF_FULL
 #define RS_WF_FULL 1  // meshes: lock-step extend one block per 256 paths, shading 64 blocks/CU (C5 49.6 -> 48.1 ms)
 #endif
-    const bool ext_spill = s->stack_need > kStackMax;
     const bool wf_full = RS_WF_FULL && s->scene_mode == kSmFlat;  // lock-step unsorted grids (meshes only)
     auto ext_grid = [&](uint32_t n) {
         const uint32_t b = (n + kBlock - 1) / kBlock;
@@ -1213,10 +1271,34 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     const uint32_t mega_blocks = wide;
     ensure_stack_overflow(s, R, (uint64_t)std::max(std::max(ext_blocks, shade_blocks), wide) * kBlock);
     const size_t n_kernel_ev = wavefront ? (size_t)n_chunks_total * st->depth : n_batches;
-    P.ev.assign(2 * (size_t)n_batches, nullptr);
-    P.kev.assign(2 * n_kernel_ev, nullptr);
+    // timing events only when the caller asks for stats (they cost a gap of ~6 us per event packet;
+    // the extend launches carry theirs in the dispatch itself, hipExtLaunchKernel)
+    P.ev.assign(timed ? 2 * (size_t)n_batches : 0, nullptr);
+    P.kev.assign(timed ? 2 * n_kernel_ev : 0, nullptr);
     for (auto& e : P.ev) HIP_OK(hipEventCreate(&e));
     for (auto& e : P.kev) HIP_OK(hipEventCreate(&e));
+    auto kev = [&](size_t i) -> hipEvent_t { return timed ? P.kev[i] : nullptr; };
+    auto record = [&](size_t i) { if (timed) HIP_OK(hipEventRecord(P.ev[i], stream)); };
+    // grid sizing from an earlier frame of the same workload (Replica::pred): bounce b's launches
+    // get enough blocks for the paths predicted there, + 1/8 + 64 blocks of slack
+#ifndef RS_GRID_PRED
+#define RS_GRID_PRED 1
+#endif
+    const uint64_t wkey = splitmix64_h(splitmix64_h(splitmix64_h((uint64_t)(uintptr_t)R.d_ds ^ ((uint64_t)W << 32 | H)) ^
+                                                    ((uint64_t)rows.begin << 40 | (uint64_t)rows.step << 20 | N)) ^
+                                       ((uint64_t)st->depth << 48 | (uint64_t)chunk));
+    if (R.hist_ev && R.hist_key && hipEventQuery(R.hist_ev) == hipSuccess) {
+        R.pred.assign(R.hist_cap / cstride, 0u);
+        for (size_t b = 0; b < R.pred.size(); ++b) R.pred[b] = R.h_hist[b * cstride + cix(0)];
+        R.pred_key = R.hist_key;
+        R.hist_key = 0;
+    }
+    const bool pred_ok = RS_GRID_PRED && sorted && R.pred_key == wkey && R.pred.size() >= st->depth;
+    auto pred_blocks = [&](uint32_t b, uint32_t full) -> uint32_t {
+        if (!pred_ok || b == 0) return full;
+        const uint64_t p = R.pred[b];
+        return (uint32_t)std::min<uint64_t>(full, (p + p / 8 + kBlock - 1) / kBlock + 64);
+    };
     const SceneRef ds = R.ref();
     HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
     if (wavefront && N > 0)
@@ -1230,61 +1312,108 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         const uint32_t nb = std::min(spb, N - s0);
         pp.s0 = s0;
         pp.n_items = (uint64_t)n_pix * nb;
-        HIP_OK(hipEventRecord(P.ev[2 * bi], stream));
+        record(2 * bi);
         if (!wavefront) {
-            HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
+            if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
             HIP_OK(launch_path_mega(ds, dc, pp, s->scene_mode, R.d_rad, R.d_cnt, mega_blocks, stream));
-            HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
+            if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
             ++ki;
             ++path_launches;
         } else {
-            for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i) {
+            if (lanes > 1) {  // fork: the lane streams start after what `stream` holds
+                HIP_OK(hipEventRecord(R.fork_ev, stream));
+                for (uint32_t l = 1; l < lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], R.fork_ev, 0));
+            }
+            uint32_t lane = 0;
+            for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i, lane = (lane + 1) % lanes) {
                 const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, pp.n_items - c0);
+                WfState WS = R.lane_ws[lane];
                 WS.counts = R.d_counts + chunk_i * (st->depth + 1) * cstride;
+                hipStream_t cs = ls[lane];
+                uint32_t** qd = R.d_qptrs[lane];
                 if (!sorted) {  // the sorted path generates camera rays inside its bounce-0 extend
-                    HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, R.d_rad, stream));
+                    HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, R.d_rad, cs));
                     ++path_launches;
                 }
                 for (uint32_t b = 0; sorted && b < st->depth; ++b) {
-                    HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
                     if (b == 0)
-                        HIP_OK(launch_wfs_gen_extend(ds, dc, pp, WS, R.d_qptrs, cstride, c0, n, R.d_rad,
-                                                     ext_grid(n), s->scene_mode, stream));
+                        HIP_OK(launch_wfs_gen_extend(ds, dc, pp, WS, qd, cstride, c0, n, R.d_rad,
+                                                     ext_grid(n), s->scene_mode, cs, kev(2 * ki), kev(2 * ki + 1)));
                     else
-                        HIP_OK(launch_wfs_extend(ds, WS, R.d_qptrs, b, cstride, pp.n_items, R.d_rad,
-                                                 ext_grid(n), s->scene_mode, stream));
-                    HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
+                        HIP_OK(launch_wfs_extend(ds, WS, qd, b, cstride, pp.n_items, R.d_rad,
+                                                 pred_blocks(b, ext_grid(n)), s->scene_mode, cs, kev(2 * ki),
+                                                 kev(2 * ki + 1)));
                     ++ki;
                     ++path_launches;
                     // (the classes' shading kernels on side streams, concurrently after the extend,
                     // measured slower: bench frame 10.24 -> 10.32 ms)
-                    for (int k = 0; k < kWfsClasses; ++k) {
-                        if (!(s->class_mask & (1u << k))) continue;  // no prim of this class: empty queue
-                        HIP_OK(launch_wfs_shade(ds, WS, R.qptr[k], k, b, cstride, st->depth, pp.n_items, R.d_rad,
-                                                std::min(wide, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
-                        ++path_launches;
+                    const uint32_t shade_grid = pred_blocks(b, std::min(wide, (n + kBlock - 1) / kBlock));
+                    if (RS_SHADE_MERGED) {
+                        // classes kShadeAllFirst .. 3 in one launch; the others (Lambertian in mode 2,
+                        // the generic class 4) in their own
+                        const uint32_t merged = s->class_mask & (0xFu & ~((1u << kShadeAllFirst) - 1u));
+                        for (int k = 0; k < kWfsClasses; ++k) {
+                            if (!(s->class_mask & (1u << k)) || (merged & (1u << k))) continue;
+                            HIP_OK(launch_wfs_shade(ds, WS, R.qptr[lane][k], k, b, cstride, st->depth, pp.n_items, R.d_rad,
+                                                    shade_grid, s->scene_mode, cs));
+                            ++path_launches;
+                        }
+                        if (merged) {
+                            HIP_OK(launch_wfs_shade_all(ds, WS, qd, merged, b, cstride, st->depth, pp.n_items,
+                                                        R.d_rad, shade_grid, s->scene_mode, cs));
+                            ++path_launches;
+                        }
+                    } else {
+                        for (int k = 0; k < kWfsClasses; ++k) {
+                            if (!(s->class_mask & (1u << k))) continue;  // no prim of this class: empty queue
+                            HIP_OK(launch_wfs_shade(ds, WS, R.qptr[lane][k], k, b, cstride, st->depth, pp.n_items, R.d_rad,
+                                                    shade_grid, s->scene_mode, cs));
+                            ++path_launches;
+                        }
                     }
                 }
+                if (sorted && chunk_i == 0 && RS_GRID_PRED) {  // chunk 0's counters for the next frame's grids
+                    const size_t words = (size_t)(st->depth + 1) * cstride;
+                    if (R.hist_cap < words) {
+                        if (R.h_hist) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipHostFree(R.h_hist)); }
+                        R.h_hist = nullptr;
+                        HIP_OK(hipHostMalloc((void**)&R.h_hist, words * sizeof(uint32_t)));
+                    }
+                    R.hist_cap = words;
+                    if (!R.hist_ev) HIP_OK(hipEventCreateWithFlags(&R.hist_ev, hipEventDisableTiming));
+                    HIP_OK(hipMemcpyAsync(R.h_hist, WS.counts, words * sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
+                    HIP_OK(hipEventRecord(R.hist_ev, cs));
+                    R.hist_key = wkey;
+                }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
-                    HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
+                    if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
                     HIP_OK(launch_wf_extend(ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock),
                                             wf_full ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
-                                            s->scene_mode, stream));
-                    HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
+                                            s->scene_mode, cs));
+                    if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
                     ++ki;
                     HIP_OK(launch_wf_shade(ds, WS, b, st->depth, pp.n_items, R.d_rad,
-                                           std::min(wf_full ? wide : shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, stream));
+                                           std::min(wf_full ? wide : shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, cs));
                     path_launches += 2;
                 }
             }
+            if (lanes > 1) {  // join: `stream` continues after every lane's chunks
+                for (uint32_t l = 1; l < lanes; ++l) {
+                    HIP_OK(hipEventRecord(R.join_ev[l], ls[l]));
+                    HIP_OK(hipStreamWaitEvent(stream, R.join_ev[l], 0));
+                }
+            }
         }
-        HIP_OK(hipEventRecord(P.ev[2 * bi + 1], stream));
+        record(2 * bi + 1);
         HIP_OK(launch_accumulate(R.d_rad, R.d_acc, n_pix, nb, s0 == 0, stream));
     }
     FinalParams fp;
     fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rows.begin; fp.row_step = rows.step; fp.n_samples = N;
     fp.gamma = st->gamma; fp.mask = d_mask;
     HIP_OK(launch_finalize(R.d_acc, d_out, fp, stream));
+    if (!R.busy) HIP_OK(hipEventCreateWithFlags(&R.busy, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(R.busy, stream));
+    R.busy_stream = stream;
     P.wavefront = wavefront;
     P.sorted = sorted;
     P.n_pix = n_pix;
@@ -1299,6 +1428,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
 // Wait for replica P's share and add its statistics into *stats (which the caller zeroed).
 void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
     if (P.empty) return;
+    if (!P.timed || !stats) { HIP_OK(hipStreamSynchronize(P.stream)); return; }
     Replica& R = *P.R;
     HIP_OK(hipMemcpyAsync(P.cnt, R.d_cnt, sizeof(P.cnt), hipMemcpyDeviceToHost, P.stream));
     const uint32_t cstride_f = P.sorted ? kWfsStride : 1;
@@ -1402,7 +1532,7 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
             const RowSet rows = replica_rows(cam, st, k, n);
             DeviceGuard g(R.device);
             if (k == 0) {
-                render_enqueue(s, R, cam, st, rows, d_mask, d_out, stream, *P[k]);
+                render_enqueue(s, R, cam, st, rows, d_mask, d_out, stream, *P[k], stats != nullptr);
                 continue;
             }
             if (rows.count() == 0) continue;
@@ -1415,7 +1545,7 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
                 HIP_OK(hipMemcpyAsync(R.d_mask, d_mask, npx, hipMemcpyDefault, R.stream));
                 m = R.d_mask;
             }
-            render_enqueue(s, R, cam, st, rows, m, R.d_out, R.stream, *P[k]);
+            render_enqueue(s, R, cam, st, rows, m, R.d_out, R.stream, *P[k], stats != nullptr);
             HIP_OK(copy_rows(d_out, R.d_out, cam->width, rows, hipMemcpyDefault, R.stream));
             HIP_OK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
             HIP_OK(hipEventRecord(done[k], R.stream));
@@ -1425,12 +1555,14 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
             for (uint32_t k = 1; k < n; ++k)
                 if (done[k]) HIP_OK(hipStreamWaitEvent(stream, done[k], 0));
         }
-        for (uint32_t k = 0; k < n; ++k) {
-            DeviceGuard g(s->reps[k]->device);
-            render_finish(s, *P[k], &acc);
+        if (stats) {  // without stats the call returns once everything is enqueued (asynchronous)
+            for (uint32_t k = 0; k < n; ++k) {
+                DeviceGuard g(s->reps[k]->device);
+                render_finish(s, *P[k], &acc);
+            }
+            DeviceGuard g(s->reps[0]->device);
+            HIP_OK(hipStreamSynchronize(stream));
         }
-        DeviceGuard g(s->reps[0]->device);
-        HIP_OK(hipStreamSynchronize(stream));
     } catch (...) {
         for (uint32_t k = 0; k < n; ++k)  // drain what was enqueued before the buffers go away
             if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipStreamSynchronize(P[k]->stream); }
@@ -1471,7 +1603,7 @@ void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
                 HIP_OK(hipMemcpyAsync(R.d_mask, mask, npx, hipMemcpyHostToDevice, R.stream));
                 m = R.d_mask;
             }
-            render_enqueue(s, R, cam, st, rows[k], m, R.d_out, R.stream, *P[k]);
+            render_enqueue(s, R, cam, st, rows[k], m, R.d_out, R.stream, *P[k], stats != nullptr);
         }
         for (uint32_t k = 0; k < n; ++k) {
             if (rows[k].count() == 0) continue;
@@ -1541,6 +1673,10 @@ int rs_scene_create(rs_scene** out) {
         if (const char* e = std::getenv("RS_MAX_BATCH_ITEMS")) {
             const unsigned long long v = std::strtoull(e, nullptr, 10);
             if (v) s->max_items_per_batch = v;
+        }
+        if (const char* e = std::getenv("RS_LANES")) {
+            const unsigned long long v = std::strtoull(e, nullptr, 10);
+            if (v) s->wf_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
         }
         *out = s;
     });

@@ -10,6 +10,10 @@ constexpr int kBlock = 256;      // 4 waves of 64
 // per-thread BVH stack entries held in LDS (24 KiB/block -> 6 blocks/CU); deeper entries spill to
 // DScene::stk_ovf, which the host sizes from the tree's exact worst-case stack depth
 constexpr int kStackMax = 24;
+#ifndef RS_LANES
+#define RS_LANES 2  // wavefront lanes: chunks of a batch in flight together on this many streams
+#endif
+constexpr uint32_t kMaxLanes = 4;
 
 // One batch of camera samples: items = n_pix_local * n_samp_batch, item -> (sample, pixel).
 // Scene modes (a template parameter of every path kernel): kSmSpheres -- world and lights are
@@ -113,11 +117,22 @@ __host__ __device__ constexpr uint32_t qsub_cap(uint32_t cap) {
 // counts[6] / counts[7] of a bounce: paths written from the front / the back of the set (light-
 // sample rays / the rest), so the next extend's waves hold rays of one kind (k_wfs_shade)
 constexpr int kCntFront = 6, kCntBack = 7;
+#ifndef RS_SHADE_MERGED
+#define RS_SHADE_MERGED 1  // shading launches per bounce: 0 one per class; 1 classes 0-3 merged; 2 classes 1-3 merged
+#endif
+constexpr int kShadeAllFirst = RS_SHADE_MERGED == 2 ? 1 : 0;
+// ev0 / ev1 (may be null): start / stop events carried by the dispatch itself (hipExtLaunchKernel:
+// no separate event packets, so timing adds no gap between kernels)
 hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
-                                uint32_t blocks, int sm, hipStream_t st);
+                                uint32_t blocks, int sm, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
-                            uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st);
+                            uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st,
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// every material class of bounce `bounce` in one launch (k_wfs_shade_all); class_mask: classes present
+hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
+                                uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,
+                                uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
                            hipStream_t st);

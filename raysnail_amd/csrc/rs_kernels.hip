@@ -10,6 +10,8 @@
 // sin/cos/pow (documented tolerance in DESIGN.md).
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "rs_device.h"
 #include "rs_internal.h"
 
@@ -42,6 +44,19 @@
     } while (0)
 
 namespace rs {
+
+// Loads through an explicit global (address space 1) pointer: the scene arrays are reached through
+// the DScene in device memory, so the compiler cannot infer their address space and emits flat
+// loads with 64-bit address arithmetic per load. With the kernel-uniform base in SGPRs and a 32-bit
+// byte offset these become `global_load ... v_off, s[base]` (one VGPR of address per load).
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+#define RS_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ T gld(const void* base, uint32_t byte_off) {
+    return *(const RS_GLOBAL T*)((const RS_GLOBAL char*)base + byte_off);
+}
 
 #ifdef RS_TRAV_STATS  // dev builds only (tools/build_variant.sh -DRS_TRAV_STATS): traversal counters
 __device__ unsigned long long g_trav_stats[8];
@@ -152,9 +167,9 @@ __device__ __forceinline__ bool slab4(float nx, float ny, float nz, float fx, fl
 // Sphere leaf during traversal: same arithmetic as sphere_t (sphere.rs:83-109) with the per-ray
 // a = |d|^2 hoisted and center_at skipped for static spheres (c + 0*t == c bit for bit).
 __device__ __forceinline__ bool sphere_t_trav(const DSphere& s, const Ray& r, double a, double tmin, double tmax,
-                                              double& t) {
+                                              double& t, bool moving = true) {
     V3 cc = ld3(s.c);
-    if (s.v[0] != 0.0 || s.v[1] != 0.0 || s.v[2] != 0.0) cc = cc + ld3(s.v) * r.time;
+    if (moving && (s.v[0] != 0.0 || s.v[1] != 0.0 || s.v[2] != 0.0)) cc = cc + ld3(s.v) * r.time;
     const V3 l = r.o - cc;
     const double half_b = dot(r.d, l);
     const double c = len2(l) - s.r2;
@@ -181,13 +196,31 @@ __device__ __forceinline__ RayC ray_consts(const Ray& r) {
     return c;
 }
 
+// A sphere record through global loads; the speed only in scenes with moving spheres
+// (DScene::moving: static spheres skip c + v*t, which is c bit for bit for v = 0)
+__device__ __forceinline__ DSphere ld_sphere(const DScene& S, const DSphere* arr, int i) {
+    const uint32_t o = (uint32_t)i * (uint32_t)sizeof(DSphere);
+    const d2v a = gld<d2v>(arr, o), b = gld<d2v>(arr, o + 16);
+    DSphere s;
+    s.c[0] = a.x; s.c[1] = a.y; s.c[2] = b.x; s.r = b.y;
+    s.r2 = gld<double>(arr, o + 32);
+    if (S.moving) {
+        s.v[0] = gld<double>(arr, o + 40);
+        const d2v c = gld<d2v>(arr, o + 48);
+        s.v[1] = c.x; s.v[2] = c.y;
+    } else {
+        s.v[0] = s.v[1] = s.v[2] = 0.0;
+    }
+    return s;
+}
+
 // Sphere leaf (leaf entry e): discriminant first, then the exact own box for spheres that hit.
 __device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int e, const Ray& r, const RayC& rc,
                                                  double tmin, double& best, double& bend, int& bp) {
     double t;
-    if (!sphere_t_trav(sp, r, rc.a, tmin, best, t)) return;
+    if (!sphere_t_trav(sp, r, rc.a, tmin, best, t, S.moving != 0)) return;
     double lo[3], hi[3];
-    if (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0) {  // host: c -/+ r (sphere.rs:117-124)
+    if (!S.moving || (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0)) {  // host: c -/+ r (sphere.rs:117-124)
         lo[0] = sp.c[0] - sp.r; lo[1] = sp.c[1] - sp.r; lo[2] = sp.c[2] - sp.r;
         hi[0] = sp.c[0] + sp.r; hi[1] = sp.c[1] + sp.r; hi[2] = sp.c[2] + sp.r;
     } else {
@@ -232,7 +265,7 @@ template <int SM>
 __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, const RayC& rc, double tmin, double& best,
                                           double& bend, int& bp) {
     if (SM == kSmSpheres) {  // prim-indexed sphere copy: no DPrim hop (e is the prim in this mode)
-        test_sphere_leaf(S, S.lsph[e], e, r, rc, tmin, best, bend, bp);
+        test_sphere_leaf(S, ld_sphere(S, S.lsph, e), e, r, rc, tmin, best, bend, bp);
         return;
     }
     if (SM == kSmFlat) {  // leaf-ordered triangle copy; its `kind` field says whether entry e is one
@@ -293,21 +326,27 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, 
 // scenes whose trees fit the LDS part never touch HBM (the bound test is one compare per push/pop).
 // The overflow address is formed only on the (rare) deep path, from the kernel-uniform base and the
 // thread's grid index, so the common path keeps no extra registers live.
-struct Stk {
+// OVF = false: the host guarantees stack_need + 3 <= kStackMax (no HBM part; the bvh4 push's three
+// unconditional writes stay inside the LDS column), so push / pop are plain LDS accesses.
+template <bool OVF>
+struct StkT {
+    static constexpr bool kOvf = OVF;
     int* lds;          // this thread's column of the block's LDS stack
     int* ovf_base;     // DScene::stk_ovf (uniform)
     __device__ __forceinline__ int* ovf(int i) const {
         return ovf_base + ((size_t)(i - kStackMax) * gridDim.x * kBlock + (size_t)blockIdx.x * kBlock + threadIdx.x);
     }
     __device__ __forceinline__ void put(int i, int v) const {
-        if (i < kStackMax) lds[i * kBlock] = v;
+        if (!OVF || i < kStackMax) lds[i * kBlock] = v;
         else *ovf(i) = v;
     }
-    __device__ __forceinline__ int get(int i) const { return i < kStackMax ? lds[i * kBlock] : *ovf(i); }
+    __device__ __forceinline__ int get(int i) const { return (!OVF || i < kStackMax) ? lds[i * kBlock] : *ovf(i); }
 };
+using Stk = StkT<true>;
 // this thread's stack (stk_all = the block's LDS array)
-__device__ __forceinline__ Stk make_stk(const DScene& S, int* stk_all) {
-    Stk s;
+template <bool OVF = true>
+__device__ __forceinline__ StkT<OVF> make_stk(const DScene& S, int* stk_all) {
+    StkT<OVF> s;
     s.lds = stk_all + threadIdx.x;
     s.ovf_base = S.stk_ovf;
     return s;
@@ -334,9 +373,9 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
 #define RS_ST_PARAMS
 #define RS_ST_PASS
 #endif
-template <int SM>
+template <int SM, class STK>
 __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const RayC& rc, const RayF4& rq, double tmin,
-                                 float tmin32, int node, int& sp, const Stk& stk, double& best, double& bend,
+                                 float tmin32, int node, int& sp, const STK& stk, double& best, double& bend,
                                  int& bp, float& best32 RS_ST_PARAMS) {
 #ifdef RS_TRAV_STATS
 #define RS_ST_LEAF4() ++st_leaves
@@ -350,14 +389,14 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
         test_leaf<SM>(S, ~(code), r, rc, tmin, best, bend, bp);                \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
-    float4 NX, FX, NY, FY, NZ, FZ;
-    int4 NC;
+    f4v NX, FX, NY, FY, NZ, FZ;
+    i4v NC;
     {
-        const char* nb = (const char*)(S.nodes4 + node);
-        NX = *(const float4*)(nb + rq.noff[0]); FX = *(const float4*)(nb + far_off(rq.noff[0], 0));
-        NY = *(const float4*)(nb + rq.noff[1]); FY = *(const float4*)(nb + far_off(rq.noff[1], 1));
-        NZ = *(const float4*)(nb + rq.noff[2]); FZ = *(const float4*)(nb + far_off(rq.noff[2], 2));
-        NC = *(const int4*)(nb + 96);
+        const uint32_t nb = (uint32_t)node * (uint32_t)sizeof(DNode4);  // < 4 GiB of nodes (host-checked)
+        NX = gld<f4v>(S.nodes4, nb + rq.noff[0]); FX = gld<f4v>(S.nodes4, nb + far_off(rq.noff[0], 0));
+        NY = gld<f4v>(S.nodes4, nb + rq.noff[1]); FY = gld<f4v>(S.nodes4, nb + far_off(rq.noff[1], 1));
+        NZ = gld<f4v>(S.nodes4, nb + rq.noff[2]); FZ = gld<f4v>(S.nodes4, nb + far_off(rq.noff[2], 2));
+        NC = gld<i4v>(S.nodes4, nb + 96u);
     }
     // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
     // and tested after the four box tests, when the node's registers are dead. Branch-free:
@@ -389,7 +428,7 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #undef RS_CS
         // the cnt - 1 farther children are pushed; inside the LDS part all three writes are
         // issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
-        if (sp + 3 <= kStackMax) {
+        if (!STK::kOvf || sp + 3 <= kStackMax) {
             stk.lds[sp * kBlock] = n0;
             stk.lds[(sp + 1) * kBlock] = n1;
             stk.lds[(sp + 2) * kBlock] = n2;
@@ -426,21 +465,21 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #undef RS_ST_LEAF4
 }
 
-template <int SM>
-__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk);
-template <int SM>
-__device__ __noinline__ int traverse_call(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
+template <int SM, class STK>
+__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk);
+template <int SM, class STK>
+__device__ __noinline__ int traverse_call(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     return traverse_body<SM>(S, r, tmin, bend_out, stk);
 }
 // inlined into the kernels of every scene mode but the generic one (a real call makes the kernel
 // keep its live registers in scratch across it: the nest-2 extend spilled 1.2 KB per lane)
-template <int SM>
-__device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
+template <int SM, class STK>
+__device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if constexpr (SM == kSmGeneric) return traverse_call<SM>(S, r, tmin, bend_out, stk);
     else return traverse_body<SM>(S, r, tmin, bend_out, stk);
 }
-template <int SM>
-__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const Stk& stk) {
+template <int SM, class STK>
+__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if (S.root < 0) return -1;
     const RayC rc = ray_consts(r);
     const RayF rf = make_rayf(r.o, rc.inv);
@@ -549,8 +588,8 @@ __device__ __forceinline__ bool finish_hit(const DScene& S, int bp, const Ray& r
     return obj_hit<SM>(S, bp, r, tmin, bend, h);
 }
 
-template <int SM>
-__device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, const Stk& stk) {
+template <int SM, class STK>
+__device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, double tmin, Hit& h, const STK& stk) {
     double bend;
     const int bp = traverse<SM>(S, r, tmin, bend, stk);
     return finish_hit<SM>(S, bp, r, tmin, bend, h);
@@ -905,7 +944,15 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
 #define RS_GEN_TILE_S 1
 #endif
 __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_t n, const PathParams& P) {
-    constexpr uint32_t S = RS_GEN_TILE_S, TW = RS_GEN_TILE_W ? RS_GEN_TILE_W : 1, TH = 64 / (TW * S), TP = TW * TH;
+    constexpr uint32_t S = RS_GEN_TILE_S, TW0 = RS_GEN_TILE_W ? RS_GEN_TILE_W : 1;
+    // A lattice with row step k (a strong-scaled share: rows r, r + k, ...) puts TH lattice rows
+    // TH * k screen rows apart: keep the tile about square on screen (step 8: 64 x 1, step 2: 16 x 4)
+    uint32_t TW = TW0, TH = 64 / (TW0 * S);
+    if (S == 1 && RS_GEN_TILE_W == 8 && P.row_step > 1) {
+        TH = P.row_step >= 8 ? 1u : P.row_step >= 4 ? 2u : 4u;
+        TW = 64u / TH;
+    }
+    const uint32_t TP = TW * TH;
     const uint32_t npl = P.n_pix_local, W = P.width;
     if (RS_GEN_TILE_W == 0 || (item0 % npl) != 0 || (n % (npl * S)) != 0) return i;
     const uint32_t grp = i / (npl * S);
@@ -1102,14 +1149,14 @@ constexpr int kClsLight = 6;
 // T = 1 and L = 0 implied for the bounce-0 shade kernels). (Writing only the hit and regenerating the
 // camera ray in the bounce-0 shade kernels instead cut 0.27 GB of HBM traffic per launch but made the
 // bench frame slower, 10.20 -> 10.26 ms: the stores are not what bounds this kernel.)
-template <bool GEN, int SM>
+template <bool GEN, int SM, bool OVF>
 __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
-    const Stk stk = make_stk(S, stk_all);
+    const StkT<OVF> stk = make_stk<OVF>(S, stk_all);
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
     const uint32_t nf = GEN ? 0u : cnt[cix(kCntFront)];
     const uint32_t n = GEN ? n_gen : nf + cnt[cix(kCntBack)];
@@ -1227,6 +1274,83 @@ __device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
 #ifndef RS_LAMB_MIN_WAVES
 #define RS_LAMB_MIN_WAVES 4  // 130 -> 128 VGPRs (4 waves/SIMD, 12 B spill): 10.01 -> 9.94 ms bench frame
 #endif
+// One batch of 256 queued paths of material class `cls` (entries base .. base + 255 of the class
+// queue, the concatenation of its kQSub sub-queues with lengths qn[], n in all): finish the hit
+// record, scatter, write the radiance of paths that end and append the survivors to the next set.
+// Must be called by every thread of the block (block_slot).
+template <int KIND, int SM>
+__device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const uint32_t* __restrict__ queue,
+                                                const uint32_t* qn, uint32_t n, uint32_t base, uint32_t bounce,
+                                                uint32_t* cnt_next, uint32_t depth, uint64_t n_items,
+                                                double* __restrict__ rad) {
+    const WfSet& cur = W.set[bounce & 1];
+    const WfSet& nxt = W.set[(bounce + 1) & 1];
+    uint32_t j = base + threadIdx.x;
+#ifdef RS_BRANCH_SORT  // measured: no gain on the bench frame (11.97 vs 11.80 ms)
+    if (KIND == RS_MAT_LAMBERTIAN || KIND == RS_MAT_DIFFUSE_METAL) {
+        // camera.rs:196-218 takes the light branch or the BSDF branch on the path's next draw
+        // (for these materials the first draw of the bounce); both are long, so peek that draw
+        // and group the block's paths by branch -- each wave then runs one branch
+        int key = 2;
+        if (j < n) {
+            Rng pk = load_rng(cur, queue[j]);
+            key = pk.gen() < 0.5 ? 0 : 1;
+        }
+        j = block_sort3(key, j);
+    }
+#endif
+    bool alive = false;
+    int light_ray = 0;
+    Ray r;
+    V3 T;
+    Rng rng;
+    uint32_t item = 0;
+    if (j < n) {
+        uint32_t g = 0, off = j;
+#pragma unroll
+        for (uint32_t k = 0; k + 1 < kQSub; ++k)
+            if (g == k && off >= qn[k]) { off -= qn[k]; g = k + 1; }
+        const uint32_t i = queue[g * W.qsub + off];
+        load_path(cur, i, r, T, rng);
+        const double2 hb = W.hit[i];
+        const int bp = (int)__double_as_longlong(hb.x);
+        Hit h;
+        finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
+        item = cur.item[i];
+        const int mi = h.mat >= 0 ? h.mat : S.default_mat;
+        const DMaterial& M0 = S.mats[mi];
+        bool cont;
+        if (KIND >= 0) {
+            cont = shade_surface<KIND, SM>(S, h, M0, M0, r, T, rng, &light_ray);
+        } else {
+            int ms = mi;
+            for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {
+                const DMaterial& X = S.mats[ms];
+                ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
+            }
+            cont = shade_surface<-1, SM>(S, h, M0, S.mats[ms], r, T, rng, &light_ray);
+        }
+        alive = cont && (bounce + 1 < depth);
+        if (!alive) {  // absorbed or depth limit: no emission term
+            const V3 L = close_path(v3(0.0, 0.0, 0.0), T);
+            rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
+        }
+    }
+    // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
+    // the front, the rest from the back: the next extend's waves then trace rays of one kind
+    uint32_t* const gc[2] = {&cnt_next[cix(kCntBack)], &cnt_next[cix(kCntFront)]};
+    const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
+    if (alive) store_path(nxt, light_ray ? slot : W.cap - 1u - slot, r, T, rng, item);
+}
+
+// the class queue's sub-queue lengths and their sum
+__device__ __forceinline__ uint32_t class_queue_len(const uint32_t* cnt, int cls, uint32_t* qn) {
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < kQSub; ++g) { qn[g] = cnt[cix(1 + cls, g)]; n += qn[g]; }
+    return n;
+}
+
 template <int KIND, int SM>
 __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest2) ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(const DScene* __restrict__ Sp, WfState W, const uint32_t* __restrict__ queue,
                                                      int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
@@ -1234,85 +1358,77 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     const uint32_t* cnt = W.counts + (size_t)bounce * stride;
     uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
-    // the class queue is kQSub sub-queues: thread j takes entry j of their concatenation
     uint32_t qn[kQSub];
-    uint32_t n = 0;
-#pragma unroll
-    for (uint32_t g = 0; g < kQSub; ++g) { qn[g] = cnt[cix(1 + cls, g)]; n += qn[g]; }
-    const WfSet& cur = W.set[bounce & 1];
-    const WfSet& nxt = W.set[(bounce + 1) & 1];
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        uint32_t j = base + threadIdx.x;
-#ifdef RS_BRANCH_SORT  // measured: no gain on the bench frame (11.97 vs 11.80 ms)
-        if (KIND == RS_MAT_LAMBERTIAN || KIND == RS_MAT_DIFFUSE_METAL) {
-            // camera.rs:196-218 takes the light branch or the BSDF branch on the path's next draw
-            // (for these materials the first draw of the bounce); both are long, so peek that draw
-            // and group the block's paths by branch -- each wave then runs one branch
-            int key = 2;
-            if (j < n) {
-                Rng pk = load_rng(cur, queue[j]);
-                key = pk.gen() < 0.5 ? 0 : 1;
-            }
-            j = block_sort3(key, j);
-        }
+    const uint32_t n = class_queue_len(cnt, cls, qn);
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock)
+        wfs_shade_batch<KIND, SM>(S, W, queue, qn, n, base, bounce, cnt_next, depth, n_items, rad);
+}
+
+// The material classes of a bounce in ONE launch (rs_host.cpp RS_SHADE_MERGED): the grid walks the
+// concatenation of the class queues' 256-path batches (class 0's, then class 1's, ...); a block's
+// class is uniform, so each batch runs its class's specialised code. One launch per bounce instead
+// of one per class removes the per-class launch tails (the small classes' queues take 5-50 us each
+// however short they are), which is what bounds the per-GPU share of a strong-scaled frame.
+// Classes kShadeAllFirst .. 3 (RS_SHADE_MERGED 1: Lambertian too; 2: Lambertian keeps its own
+// 4-wave kernel); class 4 (MixedMaterial / other, the generic material switch and the most
+// registers) keeps its own launch when a scene has it.
+constexpr int kShadeAllLast = 3;
+#ifndef RS_SHADE_ALL_WAVES
+#define RS_SHADE_ALL_WAVES 3  // 171 -> 168 VGPRs: 3 waves/SIMD
 #endif
-        bool alive = false;
-        int light_ray = 0;
-        Ray r;
-        V3 T;
-        Rng rng;
-        uint32_t item = 0;
-        if (j < n) {
-            uint32_t g = 0, off = j;
+template <int SM>
+__global__ __launch_bounds__(kBlock, RS_SHADE_ALL_WAVES) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
+                                                                              uint32_t class_mask, uint32_t bounce, uint32_t stride,
+                                                                              uint32_t depth, uint64_t n_items, double* __restrict__ rad) {
+    const DScene& S = *Sp;
+    const uint32_t* cnt = W.counts + (size_t)bounce * stride;
+    uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
+    constexpr int NC = kShadeAllLast + 1;
+    uint32_t qn[NC][kQSub], n[NC], first[NC + 1];
+    first[0] = 0;
 #pragma unroll
-            for (uint32_t k = 0; k + 1 < kQSub; ++k)
-                if (g == k && off >= qn[k]) { off -= qn[k]; g = k + 1; }
-            const uint32_t i = queue[g * W.qsub + off];
-            load_path(cur, i, r, T, rng);
-            const double2 hb = W.hit[i];
-            const int bp = (int)__double_as_longlong(hb.x);
-            Hit h;
-            finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
-            item = cur.item[i];
-            const int mi = h.mat >= 0 ? h.mat : S.default_mat;
-            const DMaterial& M0 = S.mats[mi];
-            bool cont;
-            if (KIND >= 0) {
-                cont = shade_surface<KIND, SM>(S, h, M0, M0, r, T, rng, &light_ray);
-            } else {
-                int ms = mi;
-                for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {
-                    const DMaterial& X = S.mats[ms];
-                    ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
-                }
-                cont = shade_surface<-1, SM>(S, h, M0, S.mats[ms], r, T, rng, &light_ray);
-            }
-            alive = cont && (bounce + 1 < depth);
-            if (!alive) {  // absorbed or depth limit: no emission term
-                const V3 L = close_path(v3(0.0, 0.0, 0.0), T);
-                rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
-            }
-        }
-        // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
-        // the front, the rest from the back: the next extend's waves then trace rays of one kind
-        uint32_t* const gc[2] = {&cnt_next[cix(kCntBack)], &cnt_next[cix(kCntFront)]};
-        const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
-        if (alive) store_path(nxt, light_ray ? slot : W.cap - 1u - slot, r, T, rng, item);
+    for (int k = 0; k < NC; ++k) {
+        n[k] = (k >= kShadeAllFirst && (class_mask >> k & 1u)) ? class_queue_len(cnt, k, qn[k]) : 0u;
+        first[k + 1] = first[k] + (n[k] + kBlock - 1) / kBlock;
+    }
+    for (uint32_t v = blockIdx.x; v < first[NC]; v += gridDim.x) {
+        int k = 0;
+#pragma unroll
+        for (int c = 1; c < NC; ++c) k += v >= first[c] ? 1 : 0;
+        const uint32_t base = (v - first[k]) * kBlock;
+        if (kShadeAllFirst == 0 && k == 0)
+            wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], qn[0], n[0], base, bounce, cnt_next, depth, n_items, rad);
+        else if (k == 1)
+            wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], qn[1], n[1], base, bounce, cnt_next, depth, n_items, rad);
+        else if (k == 2)
+            wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], qn[2], n[2], base, bounce, cnt_next, depth, n_items, rad);
+        else
+            wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], qn[3], n[3], base, bounce, cnt_next, depth, n_items, rad);
     }
 }
 
+// painter.rs:167-179: a pixel's sum over its samples, in sample order. One thread per (pixel,
+// channel), the batch's samples read 16 at a time (the adds stay in order): a strong-scaled share of
+// a frame has few pixels, and a thread per pixel looping over 3 x N dependent loads left the kernel
+// latency-bound (80 us for the N = 8 share of the bench frame).
 __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict__ rad, double* __restrict__ acc, uint32_t n_pix,
                                                       uint32_t n_samp, int first) {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= n_pix) return;
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= 3ull * n_pix) return;
+    const uint32_t c = (uint32_t)(t / n_pix), p = (uint32_t)(t - (uint64_t)c * n_pix);
     const uint64_t n_items = (uint64_t)n_pix * n_samp;
+    double a = first ? 0.0 : acc[(uint64_t)c * n_pix + p];
+    const double* rc = rad + (uint64_t)c * n_items + p;
+    uint32_t s = 0;
+    for (; s + 16 <= n_samp; s += 16) {
+        double v[16];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        double a = first ? 0.0 : acc[(uint64_t)c * n_pix + p];
-        const double* rc = rad + (uint64_t)c * n_items + p;
-        for (uint32_t s = 0; s < n_samp; ++s) a = a + rc[(uint64_t)s * n_pix];
-        acc[(uint64_t)c * n_pix + p] = a;
+        for (int k = 0; k < 16; ++k) v[k] = rc[(uint64_t)(s + k) * n_pix];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a = a + v[k];
     }
+    for (; s < n_samp; ++s) a = a + rc[(uint64_t)s * n_pix];
+    acc[(uint64_t)c * n_pix + p] = a;
 }
 
 __global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ acc, float* __restrict__ out, FinalParams P) {
@@ -1502,19 +1618,41 @@ hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce,
     return hipGetLastError();
 }
 
+// the LDS-only traversal stack (StkT<false>) where the tree allows it; spheres mode only (the other
+// modes keep one instantiation each: compile time)
+static bool lds_only_stack(const SceneRef& s) { return s.host->stack_need + 3 <= kStackMax; }
+#define RS_EXT_LAUNCH(GENV, ...)                                                                              \
+    RS_SM_SORTED_DISPATCH(sm, {                                                                               \
+        if constexpr (SMC == kSmSpheres) {                                                                    \
+            if (lds_only_stack(s))                                                                            \
+                hipExtLaunchKernelGGL((k_wfs_extend<GENV, SMC, false>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, __VA_ARGS__); \
+            else                                                                                              \
+                hipExtLaunchKernelGGL((k_wfs_extend<GENV, SMC, true>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, __VA_ARGS__); \
+        } else {                                                                                              \
+            hipExtLaunchKernelGGL((k_wfs_extend<GENV, SMC, true>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, __VA_ARGS__); \
+        }                                                                                                     \
+    })
 hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
-                            uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<false, SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues,
-                                                 bounce, stride, n_items, rad, DCamera{}, PathParams{}, 0ull, 0u));
+                            uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st, hipEvent_t ev0,
+                            hipEvent_t ev1) {
+    RS_EXT_LAUNCH(false, s.dev, w, queues, bounce, stride, n_items, rad, DCamera{}, PathParams{}, 0ull, 0u);
     return hipGetLastError();
 }
 
 hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
+                                uint32_t blocks, int sm, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    if (!blocks) return hipSuccess;
+    RS_EXT_LAUNCH(true, s.dev, w, queues, 0u, stride, p.n_items, rad, c, p, item0, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
+                                uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,
                                 uint32_t blocks, int sm, hipStream_t st) {
     if (!blocks) return hipSuccess;
-    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_extend<true, SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues,
-                                                 0u, stride, p.n_items, rad, c, p, item0, n));
+    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_shade_all<SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues,
+                                                 class_mask, bounce, stride, depth, n_items, rad));
     return hipGetLastError();
 }
 
@@ -1560,7 +1698,7 @@ hipError_t wf_occupancy(int sm, int* e, int* sh) {
 
 hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch, int first_batch,
                              hipStream_t st) {
-    const uint32_t blocks = (n_pix + kBlock - 1) / kBlock;
+    const uint32_t blocks = (uint32_t)((3ull * n_pix + kBlock - 1) / kBlock);
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kBlock), 0, st, rad, acc, n_pix, n_samp_batch, first_batch);
     return hipGetLastError();

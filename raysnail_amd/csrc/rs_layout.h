@@ -186,6 +186,7 @@ struct DScene {
     int32_t uv;              // 1: hit records carry (u, v) (some texture reads them: Image)
     int32_t has_media;       // 1: the scene has ConstantMedium objects (rays carry the medium key)
     int32_t stack_need;      // exact worst-case traversal stack depth of the tree in use (host-computed)
+    int32_t moving;          // 1: some sphere has a nonzero speed (center_at needs the time)
     float bg_lo[4], bg_hi[4];
 };
 

@@ -1,0 +1,10 @@
+#!/bin/bash
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r3b; mkdir -p $OUT; cd $R
+timeout -k 10 900 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 600 python tools/variant_share.py > $OUT/variants.txt 2>&1 || { echo "variants failed"; cat $OUT/variants.txt; exit 1; }
+timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/share -o share -- python3 $R/tools/share_frames.py 8 10 > $OUT/share_frames.log 2> $OUT/share.err || { echo "share trace failed"; exit 1; }
+echo done

@@ -15,6 +15,6 @@ st = photo.rows(0, 0, K).settings()
 for i in range(reps + 2):
     if i == 2:
         torch.cuda.synchronize(); t0 = time.perf_counter()
-    ds.render_device(cam.desc, st, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    ds.render_device(cam.desc, st, frame.data_ptr(), torch.cuda.current_stream().cuda_stream, stats=False)
 torch.cuda.synchronize()
 print(f"rows 0::{K}: {(time.perf_counter() - t0) / reps * 1e3:.3f} ms per share frame", flush=True)
