@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 3
+#define RS_ABI_VERSION 4
 
 /* ---- status codes ---- */
 #define RS_OK             0

@@ -186,7 +186,7 @@ def load() -> C.CDLL:
     for fn in ("rs_probe_world_hit", "rs_scene_get_info", "rs_scene_commit_devices", "rs_scene_create", "rs_scene_destroy", "rs_scene_commit", "rs_render", "rs_render_device",
                "rs_device_count"):
         getattr(lib, fn).restype = C.c_int
-    if lib.rs_abi_version() != 3:
+    if lib.rs_abi_version() != 4:
         raise RuntimeError("libraysnail_hip.so ABI mismatch")
     _LIB = lib
     return lib

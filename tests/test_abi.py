@@ -24,7 +24,7 @@ def test_header_lists_all_exports():
 def test_library_exports_every_declared_symbol(hip_lib):
     for name in header_symbols():
         assert hasattr(hip_lib, name), name
-    assert hip_lib.rs_abi_version() == 3
+    assert hip_lib.rs_abi_version() == 4
 
 
 def _scene(lib):
@@ -77,3 +77,134 @@ def test_no_lights_with_pdf_material_is_rejected_at_commit(hip_lib):
     assert lib.rs_world_add(s, h.value) == 0
     assert lib.rs_scene_commit(s) == A.RS_E_NO_LIGHTS
     lib.rs_scene_destroy(s)
+
+
+# ---------------------------------------------------------------- struct layouts ----
+# The C structs of the boundary and the #[repr(C)] mirrors a Rust caller declares.
+C_OF_RUST = {"RsTexture": "rs_texture_desc", "RsMaterial": "rs_material_desc", "RsPerlin": "rs_perlin_desc",
+             "RsTransform": "rs_transform", "RsCamera": "rs_camera_desc", "RsSettings": "rs_render_settings",
+             "RsStats": "rs_render_stats", "RsSceneInfo": "rs_scene_info", "RsNoiseStats": "rs_noise_stats"}
+LAYOUT = os.path.join(ROOT, "tests", "golden", "abi_layout.json")
+
+
+def header_structs():
+    """typedef struct name { fields } name; of the header -> [(field, array length or None)]"""
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "raysnail_hip.h")).read(), flags=re.S)
+    out = {}
+    for body, name in re.findall(r"typedef struct \w+ \{(.*?)\} (\w+);", text, flags=re.S):
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            m = re.match(r"(.*?)([\w\s,\[\]\d*]+)$", decl)
+            typ = decl.split()[0] if not decl.startswith("const") else " ".join(decl.split()[:2])
+            names = decl[len(typ):].replace("*", " ").split(",")
+            for n in names:
+                n = n.strip()
+                arr = re.match(r"(\w+)\[(\d+)\]", n)
+                fields.append((arr.group(1), int(arr.group(2))) if arr else (n, None))
+        out[name] = fields
+    return out
+
+
+def c_layout(tmp_path):
+    """offsetof / sizeof of every field of every header struct, measured by gcc"""
+    import subprocess
+    structs = header_structs()
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "raysnail_hip.h"', "int main(void) {"]
+    for name, fields in structs.items():
+        lines.append(f'printf("S {name} %zu %zu\\n", sizeof({name}), _Alignof({name}));')
+        for f, _ in fields:
+            lines.append(f'printf("F {name} {f} %zu %zu\\n", offsetof({name}, {f}), sizeof((({name}*)0)->{f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    res = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        k = line.split()
+        if k[0] == "S":
+            res.setdefault(k[1], {"fields": []}).update(size=int(k[2]), align=int(k[3]))
+        else:
+            res[k[1]]["fields"].append([k[2], int(k[3]), int(k[4])])
+    return res
+
+
+def test_c_layout_matches_committed_table(tmp_path):
+    """The layout table a foreign-language binding mirrors (tests/golden/abi_layout.json) is the
+    header's, as gcc lays it out on this ABI (x86-64 SysV, the same as the GPU box)."""
+    import json
+    got = c_layout(tmp_path)
+    if os.environ.get("RS_WRITE_ABI_LAYOUT"):
+        json.dump(got, open(LAYOUT, "w"), indent=1)
+    assert got == json.load(open(LAYOUT))
+
+
+RUST_SIZE = {"i32": (4, 4), "u32": (4, 4), "f32": (4, 4), "f64": (8, 8), "u64": (8, 8), "i64": (8, 8), "u8": (1, 1)}
+
+
+def rust_structs():
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = text[text.index("```rust"):]
+    block = block[:block.index("```", 7)]
+    out = {}
+    for name, body in re.findall(r"pub struct (\w+) \{(.*?)\}", block, flags=re.S):
+        body = re.sub(r"//[^\n]*", "", body)
+        out[name] = [(f, t.strip()) for f, t in re.findall(r"pub (\w+): ([^,]+?)(?:,|$)", body.strip())]
+    return out
+
+
+def rust_layout(structs, name, cache):
+    if name in cache:
+        return cache[name]
+    off, align, fields = 0, 1, []
+    for f, t in structs[name]:
+        arr = re.match(r"\[(\w+); (\d+)\]", t)
+        if arr:
+            sz, al = RUST_SIZE[arr.group(1)]
+            sz *= int(arr.group(2))
+        elif t.startswith("*"):
+            sz, al = 8, 8
+        elif t in RUST_SIZE:
+            sz, al = RUST_SIZE[t]
+        else:
+            sub = rust_layout(structs, t, cache)
+            sz, al = sub["size"], sub["align"]
+        off = (off + al - 1) // al * al
+        fields.append([f, off, sz])
+        off += sz
+        align = max(align, al)
+    cache[name] = {"size": (off + align - 1) // align * align, "align": align, "fields": fields}
+    return cache[name]
+
+
+def test_integration_rust_layout_matches_c():
+    """Every #[repr(C)] struct of INTEGRATION.md's FFI block has the C struct's size, alignment and
+    field offsets / sizes, field by field in order (names may differ: `type` is a Rust keyword)."""
+    import json
+    c = json.load(open(LAYOUT))
+    rs = rust_structs()
+    assert set(rs) == set(C_OF_RUST), set(rs) ^ set(C_OF_RUST)
+    assert set(C_OF_RUST.values()) == set(c)
+    cache = {}
+    for rname, cname in C_OF_RUST.items():
+        r = rust_layout(rs, rname, cache)
+        assert (r["size"], r["align"]) == (c[cname]["size"], c[cname]["align"]), rname
+        assert [f[1:] for f in r["fields"]] == [f[1:] for f in c[cname]["fields"]], rname
+
+
+def test_integration_declares_every_export():
+    """INTEGRATION.md's FFI block declares every function of the header, with its arity."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = text[text.index("```rust"):]
+    block = block[:block.index("```", 7)]
+    rust = {m.group(1): m.group(2) for m in re.finditer(r"pub fn (rs_\w+)\((.*?)\)\s*(?:->[^;]*)?;", block, flags=re.S)}
+    hdr = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "raysnail_hip.h")).read(), flags=re.S)
+    c = {m.group(1): m.group(2) for m in re.finditer(r"\b(rs_[a-z_0-9]+)\s*\(([^)]*)\)\s*;", hdr)}
+    assert set(c) == set(rust), set(c) ^ set(rust)
+    for name, args in c.items():
+        n_c = 0 if args.strip() in ("", "void") else args.count(",") + 1
+        n_r = 0 if not rust[name].strip() else rust[name].count(",") + 1
+        assert n_c == n_r, name
