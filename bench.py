@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+LANES = int(os.environ.get("RS_LANES", "2"))  # wavefront lanes of the timed region (rs_scene_set_lanes)
 
 
 def log(*a):
@@ -123,6 +124,7 @@ def main():
     cam, scene_world, _, _ = scenes.rtow_13_1(args.width, args.height)
     photo = cam.take_photo().samples(args.spp).depth(args.depth).seed(args.seed).mode(args.mode)
     ds = scene_world.device_scene()  # BVH build + upload: outside the timed region
+    ds.set_lanes(LANES)
     H, W = args.height, args.width
     frame = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     last = {}
@@ -162,7 +164,11 @@ def main():
     dt = time.perf_counter() - t0
     samples = last["samples"]
     # the dominant kernel's launches, event-timed (the events ride on the dispatches themselves), and
-    # the library's byte / segment counts: the same K frames again with stats
+    # the library's byte / segment counts: the same K frames again with stats, on ONE wavefront lane
+    # so that no launch shares the GPU with the other lane's kernels (the timed region runs two lanes,
+    # whose overlapping launches would stretch every duration); tools/isolated_kernel_stats.py reads
+    # the same isolated dispatches out of a rocprofv3 trace of this command
+    ds.set_lanes(1)
     timed["on"] = True
     kern_ms = 0.0
     kern_launches = 0
@@ -178,6 +184,7 @@ def main():
         segs += st.segments
         stat_samples += st.samples
     timed["on"] = False
+    ds.set_lanes(LANES)
     if stat_samples != samples:
         log(f"warning: stats counted {stat_samples} samples, the timed loop {samples}")
     t = torch.tensor([dt], dtype=torch.float64, device="cuda")
@@ -200,12 +207,14 @@ def main():
             render(0, 0, K, 0)
         torch.cuda.synchronize()
         sh_ms = (time.perf_counter() - t1) / args.steps * 1e3
+        ds.set_lanes(1)
         timed["on"] = True
         sh_launch_ms = 0.0
         for _ in range(args.steps):
             render(0, 0, K, 0)
             sh_launch_ms += last["stats"].kernel_ms
         timed["on"] = False
+        ds.set_lanes(LANES)
         full_ms = dt / args.steps * 1e3
         share = {"K": K, "rows": f"0::{K}", "ms_per_share": round(sh_ms, 4), "ms_full_frame": round(full_ms, 4),
                  "predicted_efficiency": round(full_ms / (K * sh_ms), 4),
@@ -228,7 +237,7 @@ def main():
                 "kernel": kname, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "alg_bytes_per_launch": int(bytes_per_launch), "launches_per_step": kern_launches // args.steps,
                 "kernel_share_of_step": round(kern_ms / args.steps / (dt / args.steps * 1e3), 4),
-                "segments_per_sample": round(segs / max(1, samples), 4)}
+                "segments_per_sample": round(segs / max(1, samples), 4), "measured_lanes": 1}
         # SURVEY 8(d)'s fixed fp32 model for the same kernel: extend reads a 28 B ray and writes a 16 B
         # hit per segment (44 B); the builder's f64 byte model above is the `frac` field
         seg_per_launch = segs / max(1, kern_launches)
@@ -247,7 +256,7 @@ def main():
             "scaling": "weak" if args.split == "passes" else "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: RTIOW final scene regenerated from seed 7 (restated ChaCha12), per-sample RNG streams",
             "config": {"workload": f"rtow_13_1 balls_scene(seed 7)+light, {W}x{H}, {n_eff} spp, depth {args.depth}",
-                       "width": W, "height": H, "spp": n_eff, "depth": args.depth, "split": args.split,
+                       "width": W, "height": H, "spp": n_eff, "depth": args.depth, "split": args.split, "lanes": LANES,
                        "samples_per_frame": W * H * n_eff, "frames_per_step": world if args.split == "passes" else 1},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -272,6 +272,10 @@ int rs_scene_commit(rs_scene* s);
  * works, rendering returns RS_E_STATE. */
 int rs_scene_commit_devices(rs_scene* s, const int* devices, int n);
 int rs_scene_get_info(const rs_scene* s, rs_scene_info* out);
+/* wavefront lanes for the scene's later renders: the chunks of a batch run round-robin on this many
+ * concurrent streams (1 .. 4; default 2, or RS_LANES at rs_scene_create). No reference counterpart
+ * (a scheduling knob like Painter::threads, painter.rs:318-325); frames are bitwise the same. */
+int rs_scene_set_lanes(rs_scene* s, uint32_t lanes);
 
 /* ---- render ---- */
 /* host output: out_rgba = W*H*4 floats; mask = W*H bytes or NULL (all pixels) */

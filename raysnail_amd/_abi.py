@@ -183,7 +183,8 @@ def load() -> C.CDLL:
     lib.rs_probe_world_hit.argtypes = [VP, VP, C.c_uint32, C.c_double, C.c_double, VP]
     lib.rs_scene_get_info.argtypes = [VP, C.POINTER(rs_scene_info)]
     lib.rs_scene_commit_devices.argtypes = [VP, C.POINTER(C.c_int), C.c_int]
-    for fn in ("rs_probe_world_hit", "rs_scene_get_info", "rs_scene_commit_devices", "rs_scene_create", "rs_scene_destroy", "rs_scene_commit", "rs_render", "rs_render_device",
+    lib.rs_scene_set_lanes.argtypes = [VP, C.c_uint32]
+    for fn in ("rs_probe_world_hit", "rs_scene_get_info", "rs_scene_set_lanes", "rs_scene_commit_devices", "rs_scene_create", "rs_scene_destroy", "rs_scene_commit", "rs_render", "rs_render_device",
                "rs_device_count"):
         getattr(lib, fn).restype = C.c_int
     if lib.rs_abi_version() != 4:
@@ -197,6 +198,6 @@ EXPORTED_SYMBOLS = [
     "rs_abi_version", "rs_last_error", "rs_device_count", "rs_stream_key", "rs_medium_uniform", "rs_scene_create",
     "rs_scene_destroy", "rs_perlin", "rs_image", "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
     "rs_difference", "rs_transformed", "rs_constant_medium", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
-    "rs_scene_commit", "rs_scene_commit_devices", "rs_scene_get_info", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
+    "rs_scene_commit", "rs_scene_commit_devices", "rs_scene_get_info", "rs_scene_set_lanes", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
     "rs_probe_world_hit", "rs_probe_samples",
 ]

@@ -548,6 +548,10 @@ class DeviceScene:
         _check(self.lib, self.lib.rs_scene_get_info(self.handle, C.byref(inf)), "rs_")
         return inf
 
+    def set_lanes(self, lanes: int) -> None:
+        """Wavefront lanes (concurrent chunk streams) for later renders (rs_scene_set_lanes)."""
+        _check(self.lib, self.lib.rs_scene_set_lanes(self.handle, lanes), "rs_")
+
     def render(self, cam: A.rs_camera_desc, st: A.rs_render_settings, mask: Optional[np.ndarray] = None,
                out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, A.rs_render_stats]:
         H, W = cam.height, cam.width

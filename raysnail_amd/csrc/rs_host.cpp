@@ -1294,6 +1294,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         R.hist_key = 0;
     }
     const bool pred_ok = RS_GRID_PRED && sorted && R.pred_key == wkey && R.pred.size() >= st->depth;
+
     auto pred_blocks = [&](uint32_t b, uint32_t full) -> uint32_t {
         if (!pred_ok || b == 0) return full;
         const uint64_t p = R.pred[b];
@@ -1387,7 +1388,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
                     if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
-                    HIP_OK(launch_wf_extend(ds, WS, b, std::min(ext_blocks, (n + kBlock - 1) / kBlock),
+                    HIP_OK(launch_wf_extend(ds, WS, b,
                                             wf_full ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
                                             s->scene_mode, cs));
                     if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
@@ -1876,6 +1877,14 @@ int rs_scene_commit_devices(rs_scene* s, const int* devices, int n) {
         commit(S(s), devices, n);
     });
 }
+int rs_scene_set_lanes(rs_scene* s, uint32_t lanes) {
+    return run([&] {
+        if (!s) throw Error(RS_E_INVALID, "null argument");
+        if (lanes < 1 || lanes > kMaxLanes) throw Error(RS_E_INVALID, "lanes must be 1 .. 4");
+        s->wf_lanes = lanes;
+    });
+}
+
 int rs_scene_get_info(const rs_scene* s, rs_scene_info* out) {
     return run([&] {
         if (!s || !out) throw Error(RS_E_INVALID, "null argument");

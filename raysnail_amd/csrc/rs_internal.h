@@ -15,6 +15,7 @@ constexpr int kStackMax = 24;
 #endif
 constexpr uint32_t kMaxLanes = 4;
 
+
 // One batch of camera samples: items = n_pix_local * n_samp_batch, item -> (sample, pixel).
 // Scene modes (a template parameter of every path kernel): kSmSpheres -- world and lights are
 // spheres only (prim-indexed sphere copy, material-sorted wavefront); kSmFlat -- spheres, rects and
@@ -86,8 +87,7 @@ hipError_t launch_path_mega(const SceneRef& s, const DCamera& c, const PathParam
                             unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st);
 hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
                          hipStream_t st);
-hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, uint32_t blocks_lockstep,
-                            int sm, hipStream_t st);
+hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st);
 // material-sorted variant (every scene mode but the generic / rich one): counts stride per bounce = kWfsStride

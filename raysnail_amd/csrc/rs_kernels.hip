@@ -15,6 +15,21 @@
 #include "rs_device.h"
 #include "rs_internal.h"
 
+// Translation units (Makefile): the scene-mode templates of the path kernels are compiled once per
+// mode, in parallel. RS_TU undefined: everything in one unit (tools/regs.sh, build_variant.sh);
+// RS_TU = -1: the common unit (mode-independent kernels, the launchers that dispatch on the scene
+// mode); RS_TU = k >= 0: scene mode k's launch_*_sm<k> instantiations only.
+#if !defined(RS_TU)
+#define RS_TU_COMMON 1
+#define RS_TU_MODES 1
+#elif RS_TU < 0
+#define RS_TU_COMMON 1
+#define RS_TU_MODES 0
+#else
+#define RS_TU_COMMON 0
+#define RS_TU_MODES 1
+#endif
+
 // the material-sorted wavefront's scene modes (rs_host.cpp: spheres, nest-0, nest-2)
 #if RS_SORTED_FLAT
 #define RS_SORTED_FLAT_CASE(...) case kSmFlat: { constexpr int SMC = kSmFlat; __VA_ARGS__; break; }
@@ -979,6 +994,7 @@ __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_
     return (grp * S + s) * npl + pl;
 }
 
+#if RS_TU_COMMON
 __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfState W, uint64_t item0, uint32_t n,
                                                    double* __restrict__ rad) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -994,6 +1010,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
     const uint32_t slot = block_slot1(live, &W.counts[0]);
     if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
 }
+#endif  // RS_TU_COMMON
 
 #ifndef RS_WF_EXT_FLAT_WAVES
 #define RS_WF_EXT_FLAT_WAVES 5  // flat scenes (meshes) are traversal-latency bound: keep 5 waves/SIMD
@@ -1017,79 +1034,6 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) v
 #ifdef RS_TRAV_STATS
         trav_stats_flush(i < n);
 #endif
-    }
-}
-
-// Persistent-lane extend for flat scenes (meshes): every lane walks its own sequence of rays
-// i, i + G, i + 2G, ... (G = grid threads) and starts the next one as soon as its current traversal
-// ends, instead of the wave stepping through rays in lock-step (where a wave runs its slowest lane's
-// traversal: on the C5 mesh the mean ray visits 42 % of its wave's node steps). The next ray's
-// records are prefetched into registers when a ray starts, so a refill waits for nothing; the f32
-// ray setup takes the f32 reciprocal of the direction (its error is far inside slab4's 2^-18 slack)
-// and the exact f64 constants are recomputed only for the rare accepted candidates (test_leaf).
-#ifndef RS_WF_PL_WAVES
-#define RS_WF_PL_WAVES 4
-#endif
-__device__ __forceinline__ RayF make_rayf_f32(const V3& o, const V3& d) {
-    RayF r;
-    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float of = (float)oo[k];
-        const float dk = fabsf(of) * 0x1p-20f + 0x1p-100f;
-        const float iv = fminf(fmaxf(1.0f / (float)dd[k], -1e30f), 1e30f);
-        r.inv[k] = iv;
-        r.opi[k] = (of + dk) * iv;
-        r.omi[k] = (of - dk) * iv;
-    }
-    return r;
-}
-template <int SM>
-__global__ __launch_bounds__(kBlock, RS_WF_PL_WAVES) void k_wf_extend_pl(const DScene* __restrict__ Sp, WfState W, uint32_t bounce) {
-    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
-    __shared__ int stk_all[kStackMax * kBlock];
-    const Stk stk = make_stk(S, stk_all);
-    const uint32_t n = W.counts[bounce];
-    const WfSet& cur = W.set[bounce & 1];
-    const uint32_t G = gridDim.x * kBlock;
-    const double tmin = 0.0001;
-    const float tmin32 = -round_up_f(-tmin);
-    uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    bool have = i < n;
-    D4 pa, pb;  // prefetched ray_o / ray_d records of ray i
-    if (have) { pa = cur.ray_o[i]; pb = cur.ray_d[i]; }
-    bool fresh = have;
-    Ray r;
-    RayF4 rq;
-    const RayC rc{};  // flat scenes' leaf tests recompute the f64 constants they need
-    int node = -1, sp = 0, bp = -1;
-    double best = RS_INF, bend = RS_INF;
-    float best32 = __builtin_huge_valf();
-#ifdef RS_TRAV_STATS
-    int st_leaves = 0;
-#endif
-    while (true) {
-        if (fresh) {  // start ray i from the prefetched records, prefetch ray i + G
-            r.o = v3(pa.x, pa.y, pa.z); r.time = pa.w;
-            r.d = v3(pb.x, pb.y, pb.z);
-            r.key = 0;
-            rq = make_rayf4(make_rayf_f32(r.o, r.d));
-            node = S.root4; sp = 0; bp = -1;
-            best = RS_INF; bend = RS_INF; best32 = __builtin_huge_valf();
-            fresh = false;
-            const uint32_t j = i + G;
-            if (j < n) { pa = cur.ray_o[j]; pb = cur.ray_d[j]; }
-        }
-        if (have) {
-            node = bvh4_step<SM>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
-            if (node < 0) {  // traversal of ray i complete: World::hit's winner and its range end
-                W.hit[i] = make_double2(__longlong_as_double((long long)(bp >= 0 ? S.lprim[bp] : -1)), bend);
-                i += G;
-                have = i < n;
-                fresh = have;
-            }
-        }
-        if (__ballot(have) == 0ull) break;
     }
 }
 
@@ -1407,6 +1351,7 @@ __global__ __launch_bounds__(kBlock, RS_SHADE_ALL_WAVES) void k_wfs_shade_all(co
     }
 }
 
+#if RS_TU_COMMON
 // painter.rs:167-179: a pixel's sum over its samples, in sample order. One thread per (pixel,
 // channel), the batch's samples read 16 at a time (the adds stay in order): a strong-scaled share of
 // a frame has few pixels, and a thread per pixel looping over 3 x N dependent loads left the kernel
@@ -1430,7 +1375,9 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict_
     for (; s < n_samp; ++s) a = a + rc[(uint64_t)s * n_pix];
     acc[(uint64_t)c * n_pix + p] = a;
 }
+#endif  // RS_TU_COMMON
 
+#if RS_TU_COMMON
 __global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ acc, float* __restrict__ out, FinalParams P) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= P.n_pix_local) return;
@@ -1448,7 +1395,9 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ 
     }
     reinterpret_cast<float4*>(out)[pix] = o;
 }
+#endif  // RS_TU_COMMON
 
+#if RS_TU_COMMON
 // ---- progressive passes (src/bin/raysnail.rs:176-208, 150-173, 394-422) ----
 __global__ __launch_bounds__(kBlock) void k_combine(float4* __restrict__ acc, const float4* __restrict__ nw, uint64_t n,
                                                    float p) {
@@ -1460,6 +1409,7 @@ __global__ __launch_bounds__(kBlock) void k_combine(float4* __restrict__ acc, co
     const float d = p + 1.0f;
     acc[i] = make_float4((o.x * p + v.x) / d, (o.y * p + v.y) / d, (o.z * p + v.z) / d, (o.w * p + v.w) / d);
 }
+#endif  // RS_TU_COMMON
 
 // one pixel's calc_noise: sum over the 5x5 window of color_diff(def, neighbour), window rows
 // y-2..y+2 (outer) and columns y-2..y+2 (inner; upstream shadows x with y), outside = def
@@ -1477,6 +1427,7 @@ __device__ __forceinline__ float calc_noise(const float4* px, int x, int y, int 
     return diff;
 }
 
+#if RS_TU_COMMON
 __global__ __launch_bounds__(kBlock) void k_noise(const float4* __restrict__ px, int w, int h, float t,
                                                  uint8_t* __restrict__ redo, unsigned int* __restrict__ mm,
                                                  unsigned long long* __restrict__ count) {
@@ -1499,33 +1450,9 @@ __global__ __launch_bounds__(kBlock) void k_noise(const float4* __restrict__ px,
     __syncthreads();
     if (threadIdx.x == 0 && s_cnt) atomicAdd(count, (unsigned long long)s_cnt);
 }
+#endif  // RS_TU_COMMON
 
-// RS_PL=1: the persistent-lane flat extend (k_wf_extend_pl) instead of the lock-step one. Measured
-// slower on the C5 mesh (59.0 vs 49.7 ms at 960x540x16, interior-only rays 297 vs 235 ms): the lanes'
-// divergence is inside each node step (leaf tests), not in finished lanes waiting for the wave.
-static bool getenv_flag_no_pl() {
-    static const int v = [] { const char* e = std::getenv("RS_PL"); return e && *e && *e != '0' ? 0 : 1; }();
-    return v != 0;
-}
-
-hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st) {
-    const uint64_t blocks = (n + kBlock - 1) / kBlock;
-    if (!blocks) return hipSuccess;
-    hipLaunchKernelGGL(k_combine, dim3((uint32_t)blocks), dim3(kBlock), 0, st, reinterpret_cast<float4*>(acc),
-                       reinterpret_cast<const float4*>(nw), n, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, unsigned int* mm,
-                        unsigned long long* count, hipStream_t st) {
-    const uint64_t n = (uint64_t)w * h;
-    const uint64_t blocks = (n + kBlock - 1) / kBlock;
-    if (!blocks) return hipSuccess;
-    hipLaunchKernelGGL(k_noise, dim3((uint32_t)blocks), dim3(kBlock), 0, st, reinterpret_cast<const float4*>(px), w, h,
-                       t, redo, mm, count);
-    return hipGetLastError();
-}
-
+#if RS_TU_COMMON
 // Diagnostic: World::hit for a batch of rays (tests/ per-primitive parity probes).
 // rays[i] = o(3) d(3) time; out[i] = hit t1 t2 p(3) n(3) 0 0 outside mat  (13 doubles, oracle layout)
 __global__ __launch_bounds__(kBlock) void k_probe_hit(const DScene* __restrict__ Sp, const double* __restrict__ rays, uint32_t n, double tmin,
@@ -1549,14 +1476,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_hit(const DScene* __restrict__
         o[11] = h.outside ? 1.0 : 0.0; o[12] = (double)h.mat;
     }
 }
-
-hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
-                            hipStream_t st) {
-    const uint32_t blocks = (n + kBlock - 1) / kBlock;
-    if (!blocks) return hipSuccess;
-    hipLaunchKernelGGL(k_probe_hit, dim3(blocks), dim3(kBlock), 0, st, s.dev, rays, n, tmin, tmax, out);
-    return hipGetLastError();
-}
+#endif  // RS_TU_COMMON
 
 // Diagnostic: the radiance and world.hit count of samples s0 .. s0+n-1 of pixel (x, y), each
 // through the megakernel's trace_path (tests/ per-sample parity; the oracle's orc_sample_radiance).
@@ -1576,21 +1496,161 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
     out[4 * (size_t)i + 3] = (double)segs;
 }
 
-hipError_t launch_probe_sample(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
-                               uint32_t s0, uint32_t n, double* out, hipStream_t st) {
+// ---- launchers ----
+// Mode-dependent launchers: launch_X_sm<SM> (defined and instantiated per mode unit) behind a
+// dispatcher on the scene mode (common unit).
+#define RS_SM_LAUNCHERS(X)                                                                                     \
+    X(hipError_t, probe_sample, (const SceneRef& s, const DCamera& c, const PathParams& p, uint32_t x, uint32_t y,  \
+                                 uint32_t s0, uint32_t n, double* out, hipStream_t st), (s, c, p, x, y, s0, n, out, st)) \
+    X(hipError_t, path_mega, (const SceneRef& s, const DCamera& c, const PathParams& p, double* rad,              \
+                              unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st),             \
+      (s, c, p, rad, seg_counters, max_blocks, st))                                                            \
+    X(hipError_t, wf_extend, (const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, hipStream_t st), \
+      (s, w, bounce, blocks, st))                                                                              \
+    X(hipError_t, wf_shade, (const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items,  \
+                             double* rad, uint32_t blocks, hipStream_t st), (s, w, bounce, depth, n_items, rad, blocks, st)) \
+    X(hipError_t, wf_occupancy, (int* e, int* sh), (e, sh))
+#define RS_SORTED_LAUNCHERS(X)                                                                                 \
+    X(hipError_t, wfs_extend, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce,   \
+                               uint32_t stride, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st,   \
+                               hipEvent_t ev0, hipEvent_t ev1),                                                \
+      (s, w, queues, bounce, stride, n_items, rad, blocks, st, ev0, ev1))                                      \
+    X(hipError_t, wfs_gen_extend, (const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,  \
+                                   uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad, \
+                                   uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1),              \
+      (s, c, p, w, queues, stride, item0, n, rad, blocks, st, ev0, ev1))                                       \
+    X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, \
+                                  uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,  \
+                                  uint32_t blocks, hipStream_t st),                                             \
+      (s, w, queues, class_mask, bounce, stride, depth, n_items, rad, blocks, st))                             \
+    X(hipError_t, wfs_shade, (const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce, \
+                              uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks,    \
+                              hipStream_t st),                                                                  \
+      (s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st))
+#define RS_DECLARE_SM(R, NAME, PARAMS, ARGS) template <int SMC> R NAME##_sm PARAMS;
+RS_SM_LAUNCHERS(RS_DECLARE_SM)
+RS_SORTED_LAUNCHERS(RS_DECLARE_SM)
+
+#if RS_TU_MODES
+template <int SMC>
+hipError_t probe_sample_sm(const SceneRef& s, const DCamera& c, const PathParams& p, uint32_t x, uint32_t y, uint32_t s0,
+                           uint32_t n, double* out, hipStream_t st) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     if (!blocks) return hipSuccess;
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_probe_sample<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, c, p, x, y, s0, n, out));
+    hipLaunchKernelGGL(k_probe_sample<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, c, p, x, y, s0, n, out);
     return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t path_mega_sm(const SceneRef& s, const DCamera& c, const PathParams& p, double* rad,
+                        unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>((p.n_items + kBlock - 1) / kBlock, max_blocks);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_path_mega<SMC>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s.dev, c, p, rad, seg_counters);
+    return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t wf_extend_sm(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce);
+    return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t wf_shade_sm(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items,
+                       double* rad, uint32_t blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_wf_shade<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, depth, n_items, rad);
+    return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t wf_occupancy_sm(int* e, int* sh) {
+    hipError_t r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<SMC>), kBlock, 0);
+    if (r == hipSuccess)
+        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<SMC>), kBlock, 0);
+    return r;
+}
+
+// the LDS-only traversal stack (StkT<false>) where the tree allows it; spheres mode only (the other
+// modes keep one instantiation each: compile time)
+[[maybe_unused]] static inline bool lds_only_stack(const SceneRef& s) { return s.host->stack_need + 3 <= kStackMax; }
+template <bool GEN, int SMC, class... A>
+static void ext_launch(const SceneRef& s, uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, A... args) {
+    if constexpr (SMC == kSmSpheres) {
+        if (lds_only_stack(s)) {
+            hipExtLaunchKernelGGL((k_wfs_extend<GEN, SMC, false>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, args...);
+            return;
+        }
+    }
+    hipExtLaunchKernelGGL((k_wfs_extend<GEN, SMC, true>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, args...);
+}
+
+template <int SMC>
+hipError_t wfs_extend_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
+                         uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    ext_launch<false, SMC>(s, blocks, st, ev0, ev1, s.dev, w, queues, bounce, stride, n_items, rad, DCamera{}, PathParams{},
+                           0ull, 0u);
+    return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t wfs_gen_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
+                             uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
+                             uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    if (!blocks) return hipSuccess;
+    ext_launch<true, SMC>(s, blocks, st, ev0, ev1, s.dev, w, queues, 0u, stride, p.n_items, rad, c, p, item0, n);
+    return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
+                            uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,
+                            uint32_t blocks, hipStream_t st) {
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL((k_wfs_shade_all<SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues, class_mask, bounce,
+                       stride, depth, n_items, rad);
+    return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t wfs_shade_sm(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
+                        uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st) {
+#define RS_SHADE_LAUNCH(KIND) \
+    hipLaunchKernelGGL((k_wfs_shade<KIND, SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, \
+                       stride, depth, n_items, rad)
+    switch (cls) {
+    case 0: RS_SHADE_LAUNCH(RS_MAT_LAMBERTIAN); break;
+    case 1: RS_SHADE_LAUNCH(RS_MAT_METAL); break;
+    case 2: RS_SHADE_LAUNCH(RS_MAT_DIFFUSE_METAL); break;
+    case 3: RS_SHADE_LAUNCH(RS_MAT_DIELECTRIC); break;
+    default: RS_SHADE_LAUNCH(-1); break;
+    }
+#undef RS_SHADE_LAUNCH
+    return hipGetLastError();
+}
+#endif  // RS_TU_MODES
+
+#if defined(RS_TU) && RS_TU >= 0  // this unit's mode
+#define RS_INSTANTIATE_SM(R, NAME, PARAMS, ARGS) template R NAME##_sm<RS_TU> PARAMS;
+RS_SM_LAUNCHERS(RS_INSTANTIATE_SM)
+#if RS_TU == 1 || RS_TU == 3 || RS_TU == 4 || (RS_SORTED_FLAT && RS_TU == 2)  // the sorted-wavefront modes
+RS_SORTED_LAUNCHERS(RS_INSTANTIATE_SM)
+#endif
+#endif
+
+#if RS_TU_COMMON
+#define RS_DISPATCH_ALL(R, NAME, PARAMS, ARGS) \
+    R launch_##NAME PARAMS_SM_##NAME { RS_SM_DISPATCH(sm, return NAME##_sm<SMC> ARGS); return hipErrorInvalidValue; }
+hipError_t launch_probe_sample(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
+                               uint32_t s0, uint32_t n, double* out, hipStream_t st) {
+    RS_SM_DISPATCH(sm, return probe_sample_sm<SMC>(s, c, p, x, y, s0, n, out, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_path_mega(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, double* rad,
                             unsigned long long* seg_counters, uint32_t max_blocks, hipStream_t st) {
-    const uint64_t blocks = std::min<uint64_t>((p.n_items + kBlock - 1) / kBlock, max_blocks);
-    if (blocks == 0) return hipSuccess;
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_path_mega<SMC>, dim3((uint32_t)blocks), dim3(kBlock), 0, st, s.dev, c, p, rad,
-                                          seg_counters));
-    return hipGetLastError();
+    RS_SM_DISPATCH(sm, return path_mega_sm<SMC>(s, c, p, rad, seg_counters, max_blocks, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w, uint64_t item0, uint32_t n, double* rad,
@@ -1601,99 +1661,75 @@ hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w
     return hipGetLastError();
 }
 
-// blocks: the resident grid (persistent lanes); blocks_lockstep: the grid of the lock-step kernel
-hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, uint32_t blocks_lockstep,
-                            int sm, hipStream_t st) {
-    if (sm == kSmFlat && s.host->root4 >= 0 && !getenv_flag_no_pl()) {
-        hipLaunchKernelGGL(k_wf_extend_pl<kSmFlat>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce);
-        return hipGetLastError();
-    }
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks_lockstep), dim3(kBlock), 0, st, s.dev, w, bounce));
-    return hipGetLastError();
+hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st) {
+    RS_SM_DISPATCH(sm, return wf_extend_sm<SMC>(s, w, bounce, blocks, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st) {
-    RS_SM_DISPATCH(sm, hipLaunchKernelGGL(k_wf_shade<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, depth, n_items, rad));
-    return hipGetLastError();
+    RS_SM_DISPATCH(sm, return wf_shade_sm<SMC>(s, w, bounce, depth, n_items, rad, blocks, st));
+    return hipErrorInvalidValue;
 }
 
-// the LDS-only traversal stack (StkT<false>) where the tree allows it; spheres mode only (the other
-// modes keep one instantiation each: compile time)
-static bool lds_only_stack(const SceneRef& s) { return s.host->stack_need + 3 <= kStackMax; }
-#define RS_EXT_LAUNCH(GENV, ...)                                                                              \
-    RS_SM_SORTED_DISPATCH(sm, {                                                                               \
-        if constexpr (SMC == kSmSpheres) {                                                                    \
-            if (lds_only_stack(s))                                                                            \
-                hipExtLaunchKernelGGL((k_wfs_extend<GENV, SMC, false>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, __VA_ARGS__); \
-            else                                                                                              \
-                hipExtLaunchKernelGGL((k_wfs_extend<GENV, SMC, true>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, __VA_ARGS__); \
-        } else {                                                                                              \
-            hipExtLaunchKernelGGL((k_wfs_extend<GENV, SMC, true>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, __VA_ARGS__); \
-        }                                                                                                     \
-    })
+hipError_t wf_occupancy(int sm, int* e, int* sh) {
+    RS_SM_DISPATCH(sm, return wf_occupancy_sm<SMC>(e, sh));
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
                             uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st, hipEvent_t ev0,
                             hipEvent_t ev1) {
-    RS_EXT_LAUNCH(false, s.dev, w, queues, bounce, stride, n_items, rad, DCamera{}, PathParams{}, 0ull, 0u);
-    return hipGetLastError();
+    RS_SM_SORTED_DISPATCH(sm, return wfs_extend_sm<SMC>(s, w, queues, bounce, stride, n_items, rad, blocks, st, ev0, ev1));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                                 uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
                                 uint32_t blocks, int sm, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    if (!blocks) return hipSuccess;
-    RS_EXT_LAUNCH(true, s.dev, w, queues, 0u, stride, p.n_items, rad, c, p, item0, n);
-    return hipGetLastError();
+    RS_SM_SORTED_DISPATCH(sm, return wfs_gen_extend_sm<SMC>(s, c, p, w, queues, stride, item0, n, rad, blocks, st, ev0, ev1));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
                                 uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,
                                 uint32_t blocks, int sm, hipStream_t st) {
-    if (!blocks) return hipSuccess;
-    RS_SM_SORTED_DISPATCH(sm, hipLaunchKernelGGL((k_wfs_shade_all<SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues,
-                                                 class_mask, bounce, stride, depth, n_items, rad));
-    return hipGetLastError();
-}
-
-template <int SM>
-static void launch_wfs_shade_sm(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
-                                uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks,
-                                hipStream_t st) {
-#define RS_SHADE_LAUNCH(KIND) \
-    hipLaunchKernelGGL((k_wfs_shade<KIND, SM>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, \
-                       stride, depth, n_items, rad)
-    switch (cls) {
-    case 0: RS_SHADE_LAUNCH(RS_MAT_LAMBERTIAN); break;
-    case 1: RS_SHADE_LAUNCH(RS_MAT_METAL); break;
-    case 2: RS_SHADE_LAUNCH(RS_MAT_DIFFUSE_METAL); break;
-    case 3: RS_SHADE_LAUNCH(RS_MAT_DIELECTRIC); break;
-    default: RS_SHADE_LAUNCH(-1); break;
-    }
-#undef RS_SHADE_LAUNCH
+    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, bounce, stride, depth, n_items, rad,
+                                                           blocks, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
                            uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
                            hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, launch_wfs_shade_sm<SMC>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st));
+    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_sm<SMC>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st));
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st) {
+    const uint64_t blocks = (n + kBlock - 1) / kBlock;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_combine, dim3((uint32_t)blocks), dim3(kBlock), 0, st, reinterpret_cast<float4*>(acc),
+                       reinterpret_cast<const float4*>(nw), n, p);
     return hipGetLastError();
 }
 
-hipError_t wf_occupancy(int sm, int* e, int* sh) {
-    hipError_t r = hipSuccess;
-    if (sm == kSmFlat && !getenv_flag_no_pl()) {
-        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend_pl<kSmFlat>), kBlock, 0);
-        if (r == hipSuccess)
-            r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<kSmFlat>), kBlock, 0);
-        return r;
-    }
-    RS_SM_DISPATCH(sm, {
-        r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<SMC>), kBlock, 0);
-        if (r == hipSuccess)
-            r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<SMC>), kBlock, 0);
-    });
-    return r;
+hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, unsigned int* mm,
+                        unsigned long long* count, hipStream_t st) {
+    const uint64_t n = (uint64_t)w * h;
+    const uint64_t blocks = (n + kBlock - 1) / kBlock;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_noise, dim3((uint32_t)blocks), dim3(kBlock), 0, st, reinterpret_cast<const float4*>(px), w, h,
+                       t, redo, mm, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
+                            hipStream_t st) {
+    const uint32_t blocks = (n + kBlock - 1) / kBlock;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_probe_hit, dim3(blocks), dim3(kBlock), 0, st, s.dev, rays, n, tmin, tmax, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch, int first_batch,
@@ -1710,10 +1746,11 @@ hipError_t launch_finalize(const double* acc, float* out_rgba, const FinalParams
     hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(kBlock), 0, st, acc, out_rgba, p);
     return hipGetLastError();
 }
+#endif  // RS_TU_COMMON
 
 }  // namespace rs
 
-#ifdef RS_TRAV_STATS
+#if defined(RS_TRAV_STATS) && RS_TU_COMMON
 extern "C" int rs_debug_trav_stats(unsigned long long out[8], int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rs::g_trav_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -3;
     if (reset) {

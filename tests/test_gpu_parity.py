@@ -290,3 +290,34 @@ def test_per_sample_radiance_vs_oracle(gpu, name):
             total += 1
     print(f"{name}: {exact}/{total} samples bit-identical, worst relative difference {worst:.3e}")
     assert worst <= 2.0 ** -40, worst
+
+
+@pytest.mark.parametrize("name", ["rtow", "example_sdl", "quadric_sdl"])
+def test_lanes_and_async_bit_identical(gpu, monkeypatch, name):
+    """Scheduling only: wavefront lanes (concurrent chunk streams, rs_scene_set_lanes), launch grids
+    sized from an earlier frame's path counts (active from the second frame of a workload on) and
+    asynchronous rs_render_device frames all give the first frame bit for bit, which equals the
+    oracle's, with the oracle's world.hit count."""
+    import torch
+    monkeypatch.setenv("RS_WF_CHUNK", "20000")         # several chunks per batch: every lane busy
+    build = {"rtow": lambda: scenes.rtow_13_1(96, 60)[:2], "example_sdl": lambda: scenes.example_sdl(96, 60),
+             "quadric_sdl": lambda: scenes.quadric_sdl(96, 60)}[name]
+    cam, world = build()
+    photo = cam.take_photo().samples(16).depth(12).seed(5)
+    ds = world.device_scene()
+    st = photo.settings()
+    ref, rstats = _oracle(world).render(cam.desc, st)
+    frames = []
+    for lanes in (1, 2, 3, 4, 1, 2):
+        ds.set_lanes(lanes)
+        img, stats = ds.render(cam.desc, st)
+        frames.append(img)
+        assert stats.segments == rstats.segments
+    out = torch.zeros((60, 96, 4), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):  # asynchronous frames back to back on one stream
+        assert ds.render_device(cam.desc, st, out.data_ptr(), s, stats=False) is None
+    torch.cuda.synchronize()
+    frames.append(out.cpu().numpy())
+    for f in frames:
+        assert np.array_equal(f, ref)
