@@ -33,26 +33,37 @@ def rows_of(rank: int, world: int, height: int) -> int:
     return (height - rank + world - 1) // world if rank < height else 0
 
 
+_ROWBUF = {}
+
+
 def gather_rows(frame: torch.Tensor, rank: int, world: int, dst: int = 0):
     """frame: (H, W, 4) with this rank's lattice rows rendered. Each rank packs its rows and sends
     them to rank `dst` (one RCCL gather at frame end), which de-interleaves them (Painter::append,
-    painter.rs:220-236). Returns the full frame on dst, None elsewhere."""
+    painter.rs:220-236). Returns the full frame on dst, None elsewhere.
+
+    Per frame: one strided copy (pack), the gather straight into a (world, per, W, 4) buffer, and on
+    dst one permuted copy into a (per * world, W, 4) frame whose rows p * world + r are rank r's p-th
+    row (the rows past H are padding). Buffers are kept across frames."""
     H = frame.shape[0]
     if world == 1:
         return frame
     per = (H + world - 1) // world
-    mine = frame[rank::world]
-    packed = torch.zeros((per,) + tuple(frame.shape[1:]), dtype=frame.dtype, device=frame.device)
-    packed[: mine.shape[0]] = mine
-    parts = [torch.empty_like(packed) for _ in range(world)] if rank == dst else None
-    dist.gather(packed, parts, dst=dst)
+    rest = tuple(frame.shape[1:])
+    key = (rest, H, frame.dtype, frame.device, rank, world, dst)
+    buf = _ROWBUF.get(key)
+    if buf is None:
+        packed = torch.zeros((per,) + rest, dtype=frame.dtype, device=frame.device)
+        allp = torch.empty((world, per) + rest, dtype=frame.dtype, device=frame.device) if rank == dst else None
+        full = torch.empty((per * world,) + rest, dtype=frame.dtype, device=frame.device) if rank == dst else None
+        _ROWBUF[key] = buf = (packed, allp, full)
+    packed, allp, full = buf
+    n = rows_of(rank, world, H)
+    packed[:n].copy_(frame[rank::world])
+    dist.gather(packed, list(allp.unbind(0)) if rank == dst else None, dst=dst)
     if rank != dst:
         return None
-    out = torch.empty_like(frame)
-    for r in range(world):
-        n = rows_of(r, world, H)
-        out[r::world] = parts[r][:n]
-    return out
+    full.view((per, world) + rest).copy_(allp.transpose(0, 1))
+    return full[:H]
 
 
 def combine_pixels(old: torch.Tensor, new: torch.Tensor, p: float) -> torch.Tensor:
