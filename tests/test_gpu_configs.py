@@ -4,7 +4,9 @@
   frames, bit for bit (the depth-8 frames are in test_gpu_parity.py);
 * C3 at its full 1920x1080 size, 256 spp, depth 50: the oracle re-renders every 90th row;
 * C5 (71.4k-triangle mesh) at 1920x1080, depth 50 at a reduced 16 spp: every 120th row;
-* C4 at 1024x1024, depth 50 at a reduced 16 spp: every 128th row.
+* C4 at 1024x1024, depth 50 at a reduced 16 spp: every 128th row;
+* the configs at full size, spp and depth: C2 every 10th row, C4 (1024 spp) every 256th, C5 (484 spp)
+  every 540th.
 Whole-frame properties (finite, alpha 1, sample count) are checked on every full-size frame.
 """
 import numpy as np
@@ -46,6 +48,27 @@ def test_sdl_scenes_depth50(gpu, name, build, spp):
     ("C4", lambda: scenes.quadric_sdl(1024, 1024), 16, 128),
 ])
 def test_full_size_config_rows_match_oracle(gpu, key, build, spp, k):
+    cam, world = build()
+    photo = cam.take_photo().samples(spp).depth(50).seed(1)
+    img = photo.shot(None, world)
+    H, W = cam.desc.height, cam.desc.width
+    n = int(spp ** 0.5) ** 2
+    assert photo.last_stats.samples == W * H * n
+    assert np.isfinite(img).all() and (img[..., 3] == 1.0).all()
+    ref, rs = _oracle(world).render(cam.desc, photo.rows(0, 0, k).settings(), threads=16)
+    assert rs.samples == len(range(0, H, k)) * W * n
+    _check(img, ref, slice(0, H, k))
+
+
+@pytest.mark.parametrize("key,build,spp,k", [
+    ("C2", lambda: scenes.example_sdl(800, 500), 64, 10),          # full size, spp and depth
+    ("C4", lambda: scenes.quadric_sdl(1024, 1024), 1024, 256),     # full 1024 spp, every 256th row
+    ("C5", lambda: scenes.mesh_scene(1920, 1080), 512, 540),       # 512 -> 484 spp (painter.rs:110-118)
+])
+def test_full_config_spp_rows_match_oracle(gpu, key, build, spp, k):
+    """The configs at their full size, spp and depth 50 (BASELINE.json configs[1], [3], [4]): the
+    whole frame on the GPU, the oracle on every k-th row (bounded CPU time: C5's mesh costs the
+    oracle ~0.15 Msamples/s)."""
     cam, world = build()
     photo = cam.take_photo().samples(spp).depth(50).seed(1)
     img = photo.shot(None, world)
