@@ -216,7 +216,8 @@ typedef struct rs_scene_info {
     uint64_t n_objects;       /* object handles (world objects, nested children, lights) */
     uint64_t n_world;         /* objects in the world list (BVH leaves) */
     int32_t  n_devices;       /* devices the scene is committed to */
-    int32_t  _pad;
+    uint32_t class_mask;      /* wavefront shading classes some world object's hits fall into (bit k: 0 Lambertian,
+                                 1 Metal, 2 DiffuseMetal, 3 Dielectric, 4 generic) */
 } rs_scene_info;
 
 typedef struct rs_scene rs_scene;

@@ -102,7 +102,7 @@ class rs_scene_info(C.Structure):
     _fields_ = [("tree_arity", C.c_int32), ("ref_order", C.c_int32), ("scene_mode", C.c_int32),
                 ("tree_depth", C.c_int32), ("stack_need", C.c_int32), ("stack_lds", C.c_int32),
                 ("n_nodes", C.c_uint64), ("n_objects", C.c_uint64), ("n_world", C.c_uint64),
-                ("n_devices", C.c_int32), ("_pad", C.c_int32)]
+                ("n_devices", C.c_int32), ("class_mask", C.c_uint32)]
 
 
 KERNEL_NAMES = {0: None, 1: "k_path_mega", 2: "k_wf_extend", 3: "k_wfs_extend"}

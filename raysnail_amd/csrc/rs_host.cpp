@@ -859,18 +859,56 @@ void build(rs_scene* s) {
         const Box3 b = s->bbox((uint32_t)h);
         for (int k = 0; k < 3; ++k) { pboxes[h].lo[k] = b.lo[k]; pboxes[h].hi[k] = b.hi[k]; }
     }
-    // wavefront shading class per prim: the material of the record its hit produces (a TfFacade
-    // passes its child's record, tf_facade.rs:41-55); CSG records take either child's material or
-    // the CSG's own (set_material_if_none, hit.rs:69-78), so they go to the generic class 4
+    // wavefront shading class per prim: the class of every material a record of its hit can carry.
+    // A TfFacade passes its child's record (tf_facade.rs:41-55); an Intersection returns either
+    // child's record with set_material_if_none (intersection.rs:81-92, hit.rs:69-78); a Difference
+    // the plus record as is or with set_material_if_none, or a back-face record carrying the minus
+    // object's own material (difference.rs:57-106). When all of them are one class the prim gets it
+    // (quadric.sdl's translated quadric-box intersections: Lambertian), else the generic class 4.
+    // Light class 6 (emission inside extend) only for leaves and TfFacades of leaves.
     std::vector<uint8_t> pclass(s->objs.size(), 4);
-    std::function<int(uint32_t)> class_of = [&](uint32_t h) -> int {
-        const HObj& o = s->objs[h];
-        if (o.kind == PK_XFORM) return class_of((uint32_t)o.a);
-        if (o.kind == PK_AND || o.kind == PK_SUB || o.kind == PK_MEDIUM) return 4;
-        const int32_t m = o.mat >= 0 ? o.mat : default_mat;
-        const int k = mats[m].kind;
+    auto mat_class = [&](int32_t m) -> int {
+        const int k = mats[m >= 0 ? m : default_mat].kind;
         return k == RS_MAT_LAMBERTIAN ? 0 : k == RS_MAT_METAL ? 1 : k == RS_MAT_DIFFUSE_METAL ? 2
              : k == RS_MAT_DIELECTRIC ? 3 : k == RS_MAT_DIFFUSE_LIGHT ? 6 : 4;
+    };
+    // record materials (RS_NO_MATERIAL = None) a hit of prim h can carry; false: unknown / media
+    std::function<bool(uint32_t, std::vector<int32_t>&)> rec_mats = [&](uint32_t h, std::vector<int32_t>& out) -> bool {
+        const HObj& o = s->objs[h];
+        if (o.kind == PK_XFORM) return rec_mats((uint32_t)o.a, out);
+        if (o.kind == PK_MEDIUM) return false;
+        if (o.kind == PK_AND || o.kind == PK_SUB) {
+            std::vector<int32_t> c;
+            if (!rec_mats((uint32_t)o.a, c)) return false;
+            if (o.kind == PK_AND && !rec_mats((uint32_t)o.b, c)) return false;
+            for (int32_t m : c) {
+                out.push_back(m != RS_NO_MATERIAL ? m : o.mat);
+                if (o.kind == PK_SUB) out.push_back(m);  // the plus record returned as is
+            }
+            if (o.kind == PK_SUB) {
+                const HObj& mo = s->objs[o.b];  // minus->material(): a leaf's own, None for composites
+                const bool leaf = mo.kind != PK_AND && mo.kind != PK_SUB && mo.kind != PK_XFORM && mo.kind != PK_MEDIUM;
+                const int32_t mm = leaf ? mo.mat : RS_NO_MATERIAL;
+                out.push_back(mm != RS_NO_MATERIAL ? mm : o.mat);
+            }
+            return true;
+        }
+        out.push_back(o.mat);
+        return true;
+    };
+    std::function<bool(uint32_t)> is_leafish = [&](uint32_t h) -> bool {
+        const HObj& o = s->objs[h];
+        if (o.kind == PK_XFORM) return is_leafish((uint32_t)o.a);
+        return o.kind != PK_AND && o.kind != PK_SUB && o.kind != PK_MEDIUM;
+    };
+    auto class_of = [&](uint32_t h) -> int {
+        std::vector<int32_t> ms;
+        if (!rec_mats(h, ms) || ms.empty()) return 4;
+        const int c0 = mat_class(ms[0]);
+        for (int32_t m : ms)
+            if (mat_class(m) != c0) return 4;
+        if (c0 == 6 && !is_leafish(h)) return 4;
+        return c0;
     };
     s->class_mask = 0;
     for (size_t h = 0; h < s->objs.size(); ++h) {
@@ -1900,6 +1938,7 @@ int rs_scene_get_info(const rs_scene* s, rs_scene_info* out) {
         out->n_objects = s->objs.size();
         out->n_world = s->world.size();
         out->n_devices = (int32_t)s->reps.size();
+        out->class_mask = s->class_mask;
     });
 }
 

@@ -1093,8 +1093,11 @@ constexpr int kClsLight = 6;
 // T = 1 and L = 0 implied for the bounce-0 shade kernels). (Writing only the hit and regenerating the
 // camera ray in the bounce-0 shade kernels instead cut 0.27 GB of HBM traffic per launch but made the
 // bench frame slower, 10.20 -> 10.26 ms: the stores are not what bounds this kernel.)
+#ifndef RS_EXT_GEN_MIN_WAVES
+#define RS_EXT_GEN_MIN_WAVES RS_EXT_MIN_WAVES  // the spheres-mode bounce-0 (camera ray) extend
+#endif
 template <bool GEN, int SM, bool OVF>
-__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
+__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : GEN ? RS_EXT_GEN_MIN_WAVES : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
                                                       uint32_t bounce, uint32_t stride, uint64_t n_items,
                                                       double* __restrict__ rad, DCamera C, PathParams P,
                                                       uint64_t item0, uint32_t n_gen) {
@@ -1266,6 +1269,14 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
         bool cont;
         if (KIND >= 0) {
             cont = shade_surface<KIND, SM>(S, h, M0, M0, r, T, rng, &light_ray);
+        } else if (M0.kind == RS_MAT_DIFFUSE_LIGHT) {
+            // a composite prim whose record carries a light material (class 4): emitted, scatter
+            // None (camera.rs:172-176, 250), 0 + T * e as in shade_step
+            const V3 e = emission<0>(S, M0, h);
+            const V3 L = v3(0.0, 0.0, 0.0) + v3(T.x * e.x, T.y * e.y, T.z * e.z);
+            rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
+            cont = false;
+            item = ~0u;  // radiance written
         } else {
             int ms = mi;
             for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {
@@ -1275,7 +1286,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
             cont = shade_surface<-1, SM>(S, h, M0, S.mats[ms], r, T, rng, &light_ray);
         }
         alive = cont && (bounce + 1 < depth);
-        if (!alive) {  // absorbed or depth limit: no emission term
+        if (!alive && item != ~0u) {  // absorbed or depth limit: no emission term
             const V3 L = close_path(v3(0.0, 0.0, 0.0), T);
             rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
         }

@@ -321,3 +321,44 @@ def test_lanes_and_async_bit_identical(gpu, monkeypatch, name):
     frames.append(out.cpu().numpy())
     for f in frames:
         assert np.array_equal(f, ref)
+
+
+def _emissive_csg_scene(w=80, h=60):
+    """Composite prims whose records carry a DiffuseLight (an Intersection with the light on the
+    CSG, a TfFacade of it) next to Lambertian CSG: the material-sorted wavefront must emit for them
+    (camera.rs:172-176, 250) although their shading class is the generic one, and Lambertian-only
+    CSG must get the Lambertian class (set_material_if_none, hit.rs:69-78)."""
+    from raysnail_amd.api import (Box, CameraBuilder, DiffuseLight, Gradient, HittableList, Intersection,
+                                  Lambertian, Sphere, TfFacade, Transform, TransformStack, World)
+    from raysnail_amd.scenes import C32
+    hl, lights = HittableList(), HittableList()
+    lamp = DiffuseLight(C32(1.0, 0.9, 0.7)).multiplier(4.0)
+    glow = Intersection(Sphere((0.0, 0.0, 0.0), 1.0, None), Box((-0.7, -0.7, -0.7), (0.7, 0.7, 0.7), None), lamp)
+    st = TransformStack()
+    st.push(Transform.translate((0.0, 2.5, 0.0)))
+    lit = TfFacade(glow, st)
+    hl.add(lit)
+    lights.add(lit)
+    lam = Lambertian(C32(0.7, 0.6, 0.5))
+    st2 = TransformStack()
+    st2.push(Transform.translate((1.5, 0.0, 0.0)))
+    hl.add(TfFacade(Intersection(Sphere((0.0, 0.0, 0.0), 1.0, None), Box((-0.8, -0.8, -0.8), (0.8, 0.8, 0.8), None), lam), st2))
+    # one child with its own (light) material, one with none: mixed classes -> generic
+    hl.add(Intersection(Sphere((-1.5, 0.0, 0.0), 1.0, DiffuseLight(C32(0.2, 0.4, 0.9))),
+                        Box((-2.3, -0.8, -0.8), (-0.7, 0.8, 0.8), None), lam))
+    hl.add(Sphere((0.0, -1001.0, 0.0), 1000.0, Lambertian(C32(0.5, 0.5, 0.5))))
+    world = World(hl, lights, Gradient(C32(0.05, 0.05, 0.1), C32(0.1, 0.1, 0.2)), (0.0, 0.0))
+    cam = CameraBuilder().look_from((0.0, 2.0, 9.0)).look_at((0.0, 0.5, 0.0)).fov(40.0).width(w).height(h).build()
+    return cam, world
+
+
+def test_emissive_and_lambertian_csg_classes(gpu):
+    cam, world = _emissive_csg_scene()
+    photo = cam.take_photo().samples(16).depth(10).seed(7)
+    img = photo.shot(None, world)
+    info = world.device_scene().info()
+    assert info.scene_mode in (3, 4)  # a nest mode: the material-sorted wavefront
+    ref, rs = _oracle(world).render(cam.desc, photo.settings())
+    assert photo.last_stats.segments == rs.segments
+    assert np.array_equal(img, ref)
+    assert img[..., :3].max() > 1.0  # the lamp is seen directly

@@ -69,3 +69,21 @@ def test_info_before_commit_is_a_state_error(hip_lib):
     assert hip_lib.rs_scene_get_info(h, C.byref(inf)) == A.RS_E_STATE
     assert hip_lib.rs_scene_commit_devices(h, None, -1) == A.RS_E_INVALID
     assert hip_lib.rs_scene_destroy(h) == 0
+
+
+def test_shading_classes_of_composites():
+    """Host-only commit (no GPU): the material-sorted wavefront's class of each world object is the
+    class of every material its hit records can carry -- quadric.sdl's translated quadric-box
+    intersections (material on the CSG, none on the children) are Lambertian; a CSG whose child
+    brings its own light material next to the CSG's Lambertian one goes to the generic class."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from raysnail_amd.api import DeviceScene
+    from raysnail_amd import scenes
+    from test_gpu_parity import _emissive_csg_scene
+    _, world = scenes.quadric_sdl(64, 64)
+    info = DeviceScene(world, devices=[]).info()
+    assert info.scene_mode == 4 and info.class_mask == 0b00001
+    _, world = _emissive_csg_scene()
+    info = DeviceScene(world, devices=[]).info()
+    assert info.class_mask == 0b10001
