@@ -1094,7 +1094,7 @@ constexpr int kClsLight = 6;
 // camera ray in the bounce-0 shade kernels instead cut 0.27 GB of HBM traffic per launch but made the
 // bench frame slower, 10.20 -> 10.26 ms: the stores are not what bounds this kernel.)
 #ifndef RS_EXT_GEN_MIN_WAVES
-#define RS_EXT_GEN_MIN_WAVES RS_EXT_MIN_WAVES  // the spheres-mode bounce-0 (camera ray) extend
+#define RS_EXT_GEN_MIN_WAVES 4  // the spheres-mode bounce-0 (camera ray) extend: 144 -> 128 VGPRs, bench frame 7.86 -> 7.63 ms
 #endif
 template <bool GEN, int SM, bool OVF>
 __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : GEN ? RS_EXT_GEN_MIN_WAVES : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
@@ -1329,10 +1329,10 @@ __global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest
 // registers) keeps its own launch when a scene has it.
 constexpr int kShadeAllLast = 3;
 #ifndef RS_SHADE_ALL_WAVES
-#define RS_SHADE_ALL_WAVES 3  // 171 -> 168 VGPRs: 3 waves/SIMD
+#define RS_SHADE_ALL_WAVES 3  // 171 -> 168 VGPRs, 3 waves/SIMD (nest-2 unbounded: 76 VGPRs would spill, C4 -21 %)
 #endif
 template <int SM>
-__global__ __launch_bounds__(kBlock, RS_SHADE_ALL_WAVES) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
+__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? 1 : RS_SHADE_ALL_WAVES) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
                                                                               uint32_t class_mask, uint32_t bounce, uint32_t stride,
                                                                               uint32_t depth, uint64_t n_items, double* __restrict__ rad) {
     const DScene& S = *Sp;
