@@ -191,14 +191,6 @@ struct Replica {
     // frame on another stream waits for it before reusing the replica's buffers
     hipEvent_t busy = nullptr;
     hipStream_t busy_stream = nullptr;
-    // launch-grid sizing: the live paths per bounce of chunk 0 of an earlier frame with the same
-    // workload key, copied back asynchronously (h_hist, hist_ev) and consumed once complete. Any grid
-    // is correct (the kernels loop grid-stride); the prediction only avoids dispatching tens of
-    // thousands of blocks that find no path (they cost ~20 us per late-bounce launch)
-    uint32_t* h_hist = nullptr; size_t hist_cap = 0;
-    hipEvent_t hist_ev = nullptr;
-    uint64_t hist_key = 0, pred_key = 0;
-    std::vector<uint32_t> pred;
 
     // the scene for a launch, with d_ds brought up to date first (it changes only when the
     // stack-overflow array is reallocated)
@@ -223,8 +215,6 @@ struct Replica {
             if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        if (h_hist) (void)hipHostFree(h_hist);
-        if (hist_ev) (void)hipEventDestroy(hist_ev);
         if (busy) (void)hipEventDestroy(busy);
         if (stream) (void)hipStreamDestroy(stream);
         if (switched) (void)hipSetDevice(prev);
@@ -1317,27 +1307,6 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     for (auto& e : P.kev) HIP_OK(hipEventCreate(&e));
     auto kev = [&](size_t i) -> hipEvent_t { return timed ? P.kev[i] : nullptr; };
     auto record = [&](size_t i) { if (timed) HIP_OK(hipEventRecord(P.ev[i], stream)); };
-    // grid sizing from an earlier frame of the same workload (Replica::pred): bounce b's launches
-    // get enough blocks for the paths predicted there, + 1/8 + 64 blocks of slack
-#ifndef RS_GRID_PRED
-#define RS_GRID_PRED 1
-#endif
-    const uint64_t wkey = splitmix64_h(splitmix64_h(splitmix64_h((uint64_t)(uintptr_t)R.d_ds ^ ((uint64_t)W << 32 | H)) ^
-                                                    ((uint64_t)rows.begin << 40 | (uint64_t)rows.step << 20 | N)) ^
-                                       ((uint64_t)st->depth << 48 | (uint64_t)chunk));
-    if (R.hist_ev && R.hist_key && hipEventQuery(R.hist_ev) == hipSuccess) {
-        R.pred.assign(R.hist_cap / cstride, 0u);
-        for (size_t b = 0; b < R.pred.size(); ++b) R.pred[b] = R.h_hist[b * cstride + cix(0)];
-        R.pred_key = R.hist_key;
-        R.hist_key = 0;
-    }
-    const bool pred_ok = RS_GRID_PRED && sorted && R.pred_key == wkey && R.pred.size() >= st->depth;
-
-    auto pred_blocks = [&](uint32_t b, uint32_t full) -> uint32_t {
-        if (!pred_ok || b == 0) return full;
-        const uint64_t p = R.pred[b];
-        return (uint32_t)std::min<uint64_t>(full, (p + p / 8 + kBlock - 1) / kBlock + 64);
-    };
     const SceneRef ds = R.ref();
     HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
     if (wavefront && N > 0)
@@ -1380,13 +1349,13 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                                                      ext_grid(n), s->scene_mode, cs, kev(2 * ki), kev(2 * ki + 1)));
                     else
                         HIP_OK(launch_wfs_extend(ds, WS, qd, b, cstride, pp.n_items, R.d_rad,
-                                                 pred_blocks(b, ext_grid(n)), s->scene_mode, cs, kev(2 * ki),
+                                                 ext_grid(n), s->scene_mode, cs, kev(2 * ki),
                                                  kev(2 * ki + 1)));
                     ++ki;
                     ++path_launches;
                     // (the classes' shading kernels on side streams, concurrently after the extend,
                     // measured slower: bench frame 10.24 -> 10.32 ms)
-                    const uint32_t shade_grid = pred_blocks(b, std::min(wide, (n + kBlock - 1) / kBlock));
+                    const uint32_t shade_grid = std::min(wide, (n + kBlock - 1) / kBlock);
                     if (RS_SHADE_MERGED) {
                         // classes kShadeAllFirst .. 3 in one launch; the others (Lambertian in mode 2,
                         // the generic class 4) in their own
@@ -1410,19 +1379,6 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                             ++path_launches;
                         }
                     }
-                }
-                if (sorted && chunk_i == 0 && RS_GRID_PRED) {  // chunk 0's counters for the next frame's grids
-                    const size_t words = (size_t)(st->depth + 1) * cstride;
-                    if (R.hist_cap < words) {
-                        if (R.h_hist) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipHostFree(R.h_hist)); }
-                        R.h_hist = nullptr;
-                        HIP_OK(hipHostMalloc((void**)&R.h_hist, words * sizeof(uint32_t)));
-                    }
-                    R.hist_cap = words;
-                    if (!R.hist_ev) HIP_OK(hipEventCreateWithFlags(&R.hist_ev, hipEventDisableTiming));
-                    HIP_OK(hipMemcpyAsync(R.h_hist, WS.counts, words * sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
-                    HIP_OK(hipEventRecord(R.hist_ev, cs));
-                    R.hist_key = wkey;
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
                     if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
