@@ -74,7 +74,7 @@ __device__ __forceinline__ T gld(const void* base, uint32_t byte_off) {
 }
 
 #ifdef RS_TRAV_STATS  // dev builds only (tools/build_variant.sh -DRS_TRAV_STATS): traversal counters
-__device__ unsigned long long g_trav_stats[8];
+__device__ unsigned long long g_trav_stats[32];  // [8 + b]: rays with 8b .. 8b+7 node steps (b < 16, last = more)
 #define RS_STAT(k, v) atomicAdd(&g_trav_stats[k], (unsigned long long)(v))
 __shared__ int s_st_nodes[256], s_st_leaves[256];
 #endif
@@ -229,6 +229,17 @@ __device__ __forceinline__ DSphere ld_sphere(const DScene& S, const DSphere* arr
     return s;
 }
 
+// A leaf-ordered triangle record (80 B) through five 16-byte global loads
+__device__ __forceinline__ LTri ld_ltri(const LTri* arr, int i) {
+    const uint32_t o = (uint32_t)i * (uint32_t)sizeof(LTri);
+    const d2v a = gld<d2v>(arr, o), b = gld<d2v>(arr, o + 16), c = gld<d2v>(arr, o + 32), d = gld<d2v>(arr, o + 48),
+              f = gld<d2v>(arr, o + 64);
+    LTri T;
+    T.p0[0] = a.x; T.p0[1] = a.y; T.p0[2] = b.x; T.a = b.y; T.b = c.x; T.c = c.y; T.d = d.x; T.e = d.y; T.f = f.x;
+    T.kind = f.y;
+    return T;
+}
+
 // Sphere leaf (leaf entry e): discriminant first, then the exact own box for spheres that hit.
 __device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int e, const Ray& r, const RayC& rc,
                                                  double tmin, double& best, double& bend, int& bp) {
@@ -284,7 +295,14 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, 
         return;
     }
     if (SM == kSmFlat) {  // leaf-ordered triangle copy; its `kind` field says whether entry e is one
+#ifndef RS_LTRI_GLD
+#define RS_LTRI_GLD 1
+#endif
+#if RS_LTRI_GLD
+        const LTri T = ld_ltri(S.ltri, e);
+#else
         const LTri& T = S.ltri[e];
+#endif
         if (T.kind == (double)PK_TRIANGLE) {
 #if defined(RS_EXP_NOLEAF)  // dev experiment (wrong frames): the cost of the triangle leaf tests
             return;
@@ -376,6 +394,7 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
         mx = max(mx, __shfl_xor(mx, off, 64));
     }
     if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); }
+    if (live) RS_STAT(8 + min(15, s_st_nodes[threadIdx.x] / 8), 1);
 }
 #endif
 // One node of the 4-wide near-first traversal: test the four child boxes of one 128-byte node,
@@ -1762,10 +1781,10 @@ hipError_t launch_finalize(const double* acc, float* out_rgba, const FinalParams
 }  // namespace rs
 
 #if defined(RS_TRAV_STATS) && RS_TU_COMMON
-extern "C" int rs_debug_trav_stats(unsigned long long out[8], int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rs::g_trav_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -3;
+extern "C" int rs_debug_trav_stats(unsigned long long out[32], int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rs::g_trav_stats), 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[32] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(rs::g_trav_stats), z, sizeof(z)) != hipSuccess) return -3;
     }
     return 0;

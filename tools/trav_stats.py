@@ -8,7 +8,7 @@ _abi.lib_path = lambda: lib_file
 import torch; torch.cuda.set_device(0)
 from raysnail_amd import scenes
 lib = _abi.load()
-out = (C.c_ulonglong * 8)()
+out = (C.c_ulonglong * 32)()
 CASES = {"rtow": (lambda: scenes.rtow_13_1(800, 500)[:2], 64, 8),
          "mesh": (lambda: scenes.mesh_scene(960, 540), 16, 50),
          "example": (lambda: scenes.example_sdl(800, 500), 16, 50),
@@ -26,3 +26,6 @@ for name in names:
     print(f"{name}: rays {rays} nodes/ray {nodes/max(rays,1):.2f} leaves/ray {leaves/max(rays,1):.2f} "
           f"wave-max nodes {wmax/max(waves,1):.2f} live lanes/wave {lanes/max(waves,1):.1f} "
           f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f}", flush=True)
+    hist = list(out[8:24])
+    tot = max(1, sum(hist))
+    print("  node steps per ray, 8-wide buckets (%):", " ".join(f"{8*b}:{100*h/tot:.1f}" for b, h in enumerate(hist)), flush=True)
