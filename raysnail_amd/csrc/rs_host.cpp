@@ -185,6 +185,9 @@ struct Replica {
     hipStream_t lane_stream[kMaxLanes] = {nullptr};  // [1..]: created on first use
     hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {nullptr};
     int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond kStackMax)
+    // phased flat-scene extend: two continuation sets per lane (ping-pong between phases)
+    void* d_cont = nullptr; size_t cont_bytes = 0;
+    ContSet cont[kMaxLanes][2]{};
     DScene* d_ds = nullptr;                 // ds in device memory (what the kernels read)
     DScene uploaded{};                      // the copy last written to d_ds
     // asynchronous frames (rs_render_device without stats): the end of the last enqueued frame, so a
@@ -208,7 +211,7 @@ struct Replica {
         if (busy) (void)hipEventSynchronize(busy);  // an asynchronous frame may still read the scene
         for (void* p : dev) (void)hipFree(p);
         for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts,
-                        (void*)d_ovf, (void*)d_ds})
+                        (void*)d_ovf, (void*)d_ds, d_cont})
             if (p) (void)hipFree(p);
         for (uint32_t l = 1; l < kMaxLanes; ++l) {
             if (lane_stream[l]) (void)hipStreamDestroy(lane_stream[l]);
@@ -236,6 +239,10 @@ struct rs_scene {
     std::vector<std::unique_ptr<Replica>> reps;   // the devices the scene is committed to, in call order
     uint64_t wf_chunk = 32ull << 20;              // RS_WF_CHUNK overrides
     uint32_t wf_lanes = RS_LANES;                 // wavefront lanes (concurrent chunk streams); RS_LANES overrides
+    // phased extend of flat scenes (k_wf_extend_ph): node-step budgets of the bounded phases, then one
+    // phase to the end; ph_n = 0 runs the one-pass extend. RS_PHASES="b0,b1,..." overrides ("0": off).
+    int ph_n = RS_PH_N;
+    int ph_budget[kMaxPhases] = {RS_PH_B0, RS_PH_B1, 0, 0};
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
     uint64_t max_items_per_batch = 32ull << 20;  // RS_MAX_BATCH_ITEMS overrides (tests)
     int tree_depth = 0;                     // levels of the tree in use
@@ -1153,6 +1160,34 @@ void carve_wf(Replica& R, uint64_t cap, uint32_t lanes) {
     }
 }
 
+// Continuation sets of the phased extend: per lane two sets of `cap` slots with `rows` stack rows.
+void carve_cont(Replica& R, uint64_t cap, uint32_t lanes, int rows) {
+    const size_t per = 4 * sizeof(int32_t) + 2 * sizeof(double) + (size_t)rows * sizeof(int32_t);
+    const size_t set_bytes = (per * cap + 8 * 256 + 255) & ~(size_t)255;
+    const size_t need = set_bytes * 2 * lanes;
+    if (need > R.cont_bytes) {
+        if (R.d_cont) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipFree(R.d_cont)); }
+        R.d_cont = nullptr;
+        R.cont_bytes = 0;
+        HIP_OK(hipMalloc(&R.d_cont, need));
+        R.cont_bytes = need;
+    }
+    auto al = [](char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); };
+    for (uint32_t l = 0; l < lanes; ++l)
+        for (int k = 0; k < 2; ++k) {
+            char* p = (char*)R.d_cont + set_bytes * (2 * l + k);
+            ContSet& c = R.cont[l][k];
+            c.idx = (uint32_t*)p; p = al(p + sizeof(uint32_t) * cap);
+            c.node = (int32_t*)p; p = al(p + sizeof(int32_t) * cap);
+            c.sp = (int32_t*)p; p = al(p + sizeof(int32_t) * cap);
+            c.bp = (int32_t*)p; p = al(p + sizeof(int32_t) * cap);
+            c.best = (double*)p; p = al(p + sizeof(double) * cap);
+            c.bend = (double*)p; p = al(p + sizeof(double) * cap);
+            c.stk = (int32_t*)p;
+            c.cap = (uint32_t)cap;
+        }
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -1265,11 +1300,18 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     const bool sorted = wavefront && (s->scene_mode == kSmSpheres || s->scene_mode == kSmNest0 ||
                                       s->scene_mode == kSmNest2 || (RS_SORTED_FLAT && s->scene_mode == kSmFlat));
     const uint32_t cstride = sorted ? kWfsStride : 1;
+    // phased extend (flat scenes with a 4-wide tree whose stack fits LDS): one continuation counter
+    // per (chunk, bounce, bounded phase), each on its own 128-byte line, after the queue counters
+    const bool phased = wavefront && !sorted && s->scene_mode == kSmFlat && s->ph_n > 0 && s->tree_arity == 4 &&
+                        s->stack_need + 3 <= kStackMax;
+    const size_t cc_base = (size_t)n_chunks_total * (st->depth + 1) * cstride;
+    const size_t n_cc = phased ? (size_t)n_chunks_total * st->depth * s->ph_n * 32 : 0;
     hipStream_t ls[kMaxLanes] = {stream};
     if (wavefront && N > 0) {
         carve_wf(R, chunk, lanes);
-        const size_t nc = (size_t)n_chunks_total * (st->depth + 1) * cstride;
+        const size_t nc = (size_t)n_chunks_total * (st->depth + 1) * cstride + n_cc;
         ensure(R.d_counts, R.counts_cap, nc);
+        if (phased) carve_cont(R, R.wf_cap, lanes, s->stack_need);
         for (uint32_t l = 1; l < lanes; ++l) {
             if (!R.lane_stream[l]) HIP_OK(hipStreamCreateWithFlags(&R.lane_stream[l], hipStreamNonBlocking));
             if (!R.join_ev[l]) HIP_OK(hipEventCreateWithFlags(&R.join_ev[l], hipEventDisableTiming));
@@ -1310,7 +1352,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     const SceneRef ds = R.ref();
     HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
     if (wavefront && N > 0)
-        HIP_OK(hipMemsetAsync(R.d_counts, 0, (size_t)n_chunks_total * (st->depth + 1) * cstride * sizeof(uint32_t), stream));
+        HIP_OK(hipMemsetAsync(R.d_counts, 0, (cc_base + n_cc) * sizeof(uint32_t), stream));
     if (N == 0) HIP_OK(hipMemsetAsync(R.d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
     uint32_t bi = 0;
     size_t ki = 0;
@@ -1382,9 +1424,24 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                 }
                 for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
                     if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
-                    HIP_OK(launch_wf_extend(ds, WS, b,
-                                            wf_full ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
-                                            s->scene_mode, cs));
+                    if (phased) {
+                        // phase 0 over the bounce's paths, phases 1.. over the previous phase's
+                        // suspended traversals (ping-pong sets), the last one to the end
+                        uint32_t* cc = R.d_counts + cc_base + ((chunk_i * st->depth + b) * s->ph_n) * 32;
+                        const uint32_t g = ext_grid(n);
+                        for (int p = 0; p <= s->ph_n; ++p) {
+                            const bool last = p == s->ph_n;
+                            HIP_OK(launch_wf_extend_ph(ds, WS, b, R.cont[lane][(p + 1) & 1], p ? cc + (p - 1) * 32 : nullptr,
+                                                       R.cont[lane][p & 1], last ? nullptr : cc + p * 32,
+                                                       last ? -1 : s->ph_budget[p], g, cs));
+                            ++path_launches;
+                        }
+                        --path_launches;
+                    } else {
+                        HIP_OK(launch_wf_extend(ds, WS, b,
+                                                wf_full ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
+                                                s->scene_mode, cs));
+                    }
                     if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
                     ++ki;
                     HIP_OK(launch_wf_shade(ds, WS, b, st->depth, pp.n_items, R.d_rad,
@@ -1668,6 +1725,16 @@ int rs_scene_create(rs_scene** out) {
         if (const char* e = std::getenv("RS_MAX_BATCH_ITEMS")) {
             const unsigned long long v = std::strtoull(e, nullptr, 10);
             if (v) s->max_items_per_batch = v;
+        }
+        if (const char* e = std::getenv("RS_PHASES")) {
+            s->ph_n = 0;
+            for (const char* q = e; *q && s->ph_n < kMaxPhases;) {
+                char* end = nullptr;
+                const long v = std::strtol(q, &end, 10);
+                if (end == q || v <= 0) break;
+                s->ph_budget[s->ph_n++] = (int)v;
+                q = (*end == ',' || *end == '/') ? end + 1 : end;
+            }
         }
         if (const char* e = std::getenv("RS_LANES")) {
             const unsigned long long v = std::strtoull(e, nullptr, 10);

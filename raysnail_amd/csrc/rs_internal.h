@@ -14,6 +14,15 @@ constexpr int kStackMax = 24;
 #define RS_LANES 2  // wavefront lanes: chunks of a batch in flight together on this many streams
 #endif
 constexpr uint32_t kMaxLanes = 4;
+#ifndef RS_PH_N
+#define RS_PH_N 0     // phased flat-scene extend: bounded phases by default (RS_PHASES overrides)
+#endif
+#ifndef RS_PH_B0
+#define RS_PH_B0 24   // node-step budget of phase 0
+#endif
+#ifndef RS_PH_B1
+#define RS_PH_B1 16
+#endif
 
 
 // One batch of camera samples: items = n_pix_local * n_samp_batch, item -> (sample, pixel).
@@ -90,6 +99,26 @@ hipError_t launch_wf_gen(const DCamera& c, const PathParams& p, const WfState& w
 hipError_t launch_wf_extend(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, int sm, hipStream_t st);
 hipError_t launch_wf_shade(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items, double* rad,
                            uint32_t blocks, int sm, hipStream_t st);
+// Suspended traversals of the phased flat-scene extend (k_wf_extend_ph), SoA over cap slots: the
+// path's slot in the bounce's set, the next node, stack depth, best leaf entry, range end and the
+// accepted range end; stack entry k of slot j at stk[k * cap + j].
+struct ContSet {
+    uint32_t* idx;
+    int32_t* node;
+    int32_t* sp;
+    int32_t* bp;
+    double* best;
+    double* bend;
+    int32_t* stk;
+    uint32_t cap;
+};
+constexpr int kMaxPhases = 4;
+// One phase of a flat scene's extend at `bounce`: in_cnt == nullptr starts every path of the bounce,
+// otherwise the in_cnt suspended traversals of `in` are resumed; each runs at most `budget` node
+// steps (budget < 0: to the end) and the ones still open are appended to `out` / out_cnt.
+hipError_t launch_wf_extend_ph(const SceneRef& s, const WfState& w, uint32_t bounce, const ContSet& in,
+                               const uint32_t* in_cnt, const ContSet& out, uint32_t* out_cnt, int budget, uint32_t blocks,
+                               hipStream_t st);
 // material-sorted variant (every scene mode but the generic / rich one): counts stride per bounce = kWfsStride
 #ifndef RS_SORTED_FLAT
 #define RS_SORTED_FLAT 0  // flat scenes (meshes) on the material-sorted wavefront too

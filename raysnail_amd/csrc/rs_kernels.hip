@@ -76,7 +76,7 @@ __device__ __forceinline__ T gld(const void* base, uint32_t byte_off) {
 #ifdef RS_TRAV_STATS  // dev builds only (tools/build_variant.sh -DRS_TRAV_STATS): traversal counters
 __device__ unsigned long long g_trav_stats[32];  // [8 + b]: rays with 8b .. 8b+7 node steps (b < 16, last = more)
 #define RS_STAT(k, v) atomicAdd(&g_trav_stats[k], (unsigned long long)(v))
-__shared__ int s_st_nodes[256], s_st_leaves[256];
+__shared__ int s_st_nodes[256], s_st_leaves[256], s_st_witer[256];
 #endif
 
 // aabb.rs:20-38 with inv = 1/d[i] precomputed per ray (the reference recomputes the same value
@@ -393,7 +393,9 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
         n += __shfl_xor(n, off, 64); l += __shfl_xor(l, off, 64); cnt += __shfl_xor(cnt, off, 64);
         mx = max(mx, __shfl_xor(mx, off, 64));
     }
-    if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); }
+    int wi = live ? s_st_witer[threadIdx.x] : 0;  // the wave's leaf-loop passes: the max over its lanes
+    for (int off = 32; off > 0; off >>= 1) wi = max(wi, __shfl_xor(wi, off, 64));
+    if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); RS_STAT(6, wi); }
     if (live) RS_STAT(8 + min(15, s_st_nodes[threadIdx.x] / 8), 1);
 }
 #endif
@@ -401,8 +403,8 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
 // push the farther inner children, test the node's leaves; returns the next node (-1: done).
 // Shared by traverse() and the persistent-lane flat-scene extend (k_wf_extend_pl).
 #ifdef RS_TRAV_STATS
-#define RS_ST_PARAMS , int& st_leaves
-#define RS_ST_PASS , st_leaves
+#define RS_ST_PARAMS , int& st_leaves, int& st_witer
+#define RS_ST_PASS , st_leaves, st_witer
 #else
 #define RS_ST_PARAMS
 #define RS_ST_PASS
@@ -449,6 +451,12 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
     }
     RS_SLOT(x, n0, e0, l0) RS_SLOT(y, n1, e1, l1) RS_SLOT(z, n2, e2, l2) RS_SLOT(w, n3, e3, l3)
 #undef RS_SLOT
+#ifdef RS_TRAV_STATS
+    {   // leaf-loop passes of the wave at this node (the active lanes' maximum leaf count)
+        const int nl = (l0 != INT32_MIN) + (l1 != INT32_MIN) + (l2 != INT32_MIN) + (l3 != INT32_MIN);
+        for (int q = 1; q <= 4; ++q) st_witer += __ballot(nl >= q) != 0ull;
+    }
+#endif
     const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
                     (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
     int next;
@@ -499,6 +507,140 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #undef RS_ST_LEAF4
 }
 
+// ---- flat scenes (meshes): node steps and leaf tests in separate wave passes ----
+// In bvh4_step a wave runs each node's leaf loop as long as the lane with the most leaves there, and
+// its other lanes idle through the f64 triangle tests (the lanes' divergence sits inside the node
+// steps). Here a lane's leaf entries go to a FIFO of RS_LEAFQ entries in LDS instead, and the wave
+// chooses, pass by pass: a leaf pass (every lane with a queued entry tests its oldest one) when at
+// least RS_LEAFQ_THR/64 of its working lanes have one queued or no lane can take a node step;
+// otherwise a node step for the lanes with room for four more entries. The choice is wave-uniform
+// (ballots), so neither pass diverges on it.
+// Same hit as traverse(): a lane tests its entries in the order it met them, only later (a node step
+// culls with the range the tests so far left, a superset of the nodes bvh4_step visits), and flat
+// scenes' objects are monotone -- a later test sees a range at least as large, the closest entry wins
+// whatever the order (equal t: the first met, as before), and the winner's record needs only a range
+// end above its own t.
+#ifndef RS_LEAFQ
+#define RS_LEAFQ 8      // entries per lane (power of two, >= 8)
+#endif
+#ifndef RS_LEAFQ_THR
+#define RS_LEAFQ_THR 48  // leaf pass at >= 48/64 of the working lanes with an entry queued
+#endif
+#ifndef RS_FLAT_LEAFQ
+#define RS_FLAT_LEAFQ 1
+#endif
+template <int SM, class STK>
+__device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, float tmin32, float best32, int node, int& sp,
+                                           const STK& stk, int* q, int& qt) {
+    f4v NX, FX, NY, FY, NZ, FZ;
+    i4v NC;
+    {
+        const uint32_t nb = (uint32_t)node * (uint32_t)sizeof(DNode4);
+        NX = gld<f4v>(S.nodes4, nb + rq.noff[0]); FX = gld<f4v>(S.nodes4, nb + far_off(rq.noff[0], 0));
+        NY = gld<f4v>(S.nodes4, nb + rq.noff[1]); FY = gld<f4v>(S.nodes4, nb + far_off(rq.noff[1], 1));
+        NZ = gld<f4v>(S.nodes4, nb + rq.noff[2]); FZ = gld<f4v>(S.nodes4, nb + far_off(rq.noff[2], 2));
+        NC = gld<i4v>(S.nodes4, nb + 96u);
+    }
+    int n0, n1, n2, n3, l0, l1, l2, l3;
+    float e0, e1, e2, e3;
+#define RS_SLOT(K, NK, EK, LK)                                                                \
+    {                                                                                 \
+        float e;                                                                      \
+        const int c = NC.K;                                                           \
+        const bool hk = slab4(NX.K, NY.K, NZ.K, FX.K, FY.K, FZ.K, rq, tmin32, best32, e) & (c != INT32_MIN); \
+        LK = (hk & (c < 0)) ? c : INT32_MIN;                                          \
+        NK = c;                                                                       \
+        EK = (hk & (c >= 0)) ? e : -__builtin_huge_valf();                            \
+    }
+    RS_SLOT(x, n0, e0, l0) RS_SLOT(y, n1, e1, l1) RS_SLOT(z, n2, e2, l2) RS_SLOT(w, n3, e3, l3)
+#undef RS_SLOT
+    // the leaf entries, in slot order, to the lane's FIFO: four unconditional writes at the tail (the
+    // caller guarantees four free entries), the tail advanced past the real ones
+    {
+        constexpr int M = RS_LEAFQ - 1;
+        int k = qt;
+        q[(k & M) * kBlock] = l0; k += l0 != INT32_MIN;
+        q[(k & M) * kBlock] = l1; k += l1 != INT32_MIN;
+        q[(k & M) * kBlock] = l2; k += l2 != INT32_MIN;
+        q[(k & M) * kBlock] = l3; k += l3 != INT32_MIN;
+        qt = k;
+    }
+    const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
+                    (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
+    int next;
+    if (cnt == 0) {
+        next = -1;
+        if (sp > 0) { --sp; next = stk.get(sp); }
+    } else {
+#define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
+        RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
+#undef RS_CS
+        if (!STK::kOvf || sp + 3 <= kStackMax) {
+            stk.lds[sp * kBlock] = n0;
+            stk.lds[(sp + 1) * kBlock] = n1;
+            stk.lds[(sp + 2) * kBlock] = n2;
+        } else {
+            if (cnt > 1) stk.put(sp, n0);
+            if (cnt > 2) stk.put(sp + 1, n1);
+            if (cnt > 3) stk.put(sp + 2, n2);
+        }
+        sp += cnt - 1;
+        next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
+    }
+    return next;
+}
+
+// World::hit of a flat scene with a 4-wide tree through queued leaf passes (above). q: this lane's
+// column of the block's FIFO array (RS_LEAFQ x kBlock ints). Every lane of the wave that calls it
+// must call it (the pass choice is a ballot over the calling lanes).
+template <int SM, class STK>
+__device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk,
+                                               int* q) {
+    const RayC rc = ray_consts(r);
+    const RayF4 rq = make_rayf4(make_rayf(r.o, rc.inv));
+    const float tmin32 = -round_up_f(-tmin);
+    double best = RS_INF, bend = RS_INF;
+    float best32 = __builtin_huge_valf();
+    int bp = -1, node = S.root4, sp = 0, qh = 0, qt = 0;
+#ifdef RS_TRAV_STATS
+    int st_nodes = 0, st_leaves = 0, st_witer = 0;
+#endif
+    while (true) {
+        const bool has_leaf = qt != qh;
+        const bool can_node = node >= 0 && qt - qh <= RS_LEAFQ - 4;
+        const uint64_t work = __ballot(node >= 0 || has_leaf);
+        if (work == 0ull) break;
+        const uint64_t lm = __ballot(has_leaf);
+        if (__popcll(lm) * 64 >= RS_LEAFQ_THR * __popcll(work) || __ballot(can_node) == 0ull) {
+#ifdef RS_TRAV_STATS
+            ++st_witer;
+#endif
+            if (has_leaf) {
+                const int code = q[(qh & (RS_LEAFQ - 1)) * kBlock];
+                ++qh;
+#ifdef RS_TRAV_STATS
+                ++st_leaves;
+#endif
+                const int bp_prev = bp;
+                test_leaf<SM>(S, ~code, r, rc, tmin, best, bend, bp);
+                if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);
+            }
+        } else if (can_node) {
+#ifdef RS_TRAV_STATS
+            ++st_nodes;
+#endif
+            node = bvh4_node_q<SM>(S, rq, tmin32, best32, node, sp, stk, q, qt);
+        }
+    }
+#ifdef RS_TRAV_STATS
+    s_st_nodes[threadIdx.x] = st_nodes;
+    s_st_leaves[threadIdx.x] = st_leaves;
+    s_st_witer[threadIdx.x] = st_witer;
+#endif
+    bend_out = bend;
+    return bp >= 0 ? S.lprim[bp] : bp;
+}
+
 template <int SM, class STK>
 __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk);
 template <int SM, class STK>
@@ -524,7 +666,7 @@ __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, doub
     int node = S.root;
     int sp = 0;
 #ifdef RS_TRAV_STATS
-    int st_nodes = 0, st_leaves = 0;
+    int st_nodes = 0, st_leaves = 0, st_witer = 0;
 #define RS_ST_NODE() ++st_nodes
 #define RS_ST_LEAF() ++st_leaves
 #else
@@ -605,6 +747,7 @@ __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, doub
 #ifdef RS_TRAV_STATS
     s_st_nodes[threadIdx.x] = st_nodes;   // reduced per wave by the kernel (rs_trav_stats_flush)
     s_st_leaves[threadIdx.x] = st_leaves;
+    s_st_witer[threadIdx.x] = st_witer;
 #endif
     bend_out = bend;
     return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
@@ -1039,6 +1182,9 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) v
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const Stk stk = make_stk(S, stk_all);
+#if RS_FLAT_LEAFQ
+    __shared__ int leafq[SM == kSmFlat ? RS_LEAFQ * kBlock : 1];
+#endif
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -1047,12 +1193,79 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) v
             Ray r = load_ray(cur, i);
             if (rich_of(SM) && S.has_media) r.key = load_rng(cur, i).medium_key();  // the segment's medium key
             double bend = RS_INF;
-            const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
+            int bp;
+#if RS_FLAT_LEAFQ
+            if (SM == kSmFlat && S.root4 >= 0)
+                bp = traverse_flat_q<SM>(S, r, 0.0001, bend, stk, leafq + threadIdx.x);
+            else
+#endif
+                bp = traverse<SM>(S, r, 0.0001, bend, stk);
             W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
         }
 #ifdef RS_TRAV_STATS
         trav_stats_flush(i < n);
 #endif
+    }
+}
+
+// ---- phased extend (flat scenes) ----
+// A lock-step wave runs the union of its lanes' traversal loops, and mesh rays differ by 10x in node
+// steps (profiles/r3/trav_stats_histogram.txt: mean 17.8, wave maximum 40.9 on the C5 mesh). Phase 0
+// runs every path of the bounce for at most `budget` 4-wide node steps; the traversals still open are
+// suspended -- next node, stack, best entry and range ends -- into a compacted continuation set, and
+// the next phase resumes them in full waves. A resumed traversal continues the same sequence of node
+// steps (best32 is a function of best and bp), so the hit is the one traverse() returns.
+template <int SM, class STK>
+__device__ __forceinline__ bool trav4_run(const DScene& S, const Ray& r, double tmin, int& node, int& sp, double& best,
+                                          double& bend, int& bp, const STK& stk, int budget) {
+    const RayC rc = ray_consts(r);
+    const RayF4 rq = make_rayf4(make_rayf(r.o, rc.inv));
+    const float tmin32 = -round_up_f(-tmin);
+    float best32 = bp >= 0 ? round_up_f(best) : __builtin_huge_valf();
+#ifdef RS_TRAV_STATS
+    int st_leaves = 0, st_witer = 0;
+#endif
+    for (int k = 0; node >= 0; ++k) {
+        if (k == budget) return false;
+        node = bvh4_step<SM>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
+    }
+    return true;
+}
+
+#ifndef RS_WF_PH_WAVES
+#define RS_WF_PH_WAVES RS_WF_EXT_FLAT_WAVES
+#endif
+template <int SM>
+__global__ __launch_bounds__(kBlock, RS_WF_PH_WAVES) void k_wf_extend_ph(const DScene* __restrict__ Sp, WfState W, uint32_t bounce,
+                                                                          ContSet in, const uint32_t* __restrict__ in_cnt,
+                                                                          ContSet out, uint32_t* __restrict__ out_cnt, int budget) {
+    const DScene& S = *Sp;
+    __shared__ int stk_all[kStackMax * kBlock];
+    const StkT<false> stk = make_stk<false>(S, stk_all);  // the host enables phases for LDS-only stacks
+    const uint32_t n = in_cnt ? *in_cnt : W.counts[bounce];
+    if (blockIdx.x * kBlock >= n) return;  // whole block past the end (uniform, before the queue barriers)
+    const WfSet& cur = W.set[bounce & 1];
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    bool open = false;
+    uint32_t i = 0;
+    int node = S.root4, sp = 0, bp = -1;
+    double best = RS_INF, bend = RS_INF;
+    if (j < n) {
+        i = j;
+        if (in_cnt) {
+            i = in.idx[j]; node = in.node[j]; sp = in.sp[j]; bp = in.bp[j]; best = in.best[j]; bend = in.bend[j];
+            for (int k = 0; k < sp; ++k) stk.lds[k * kBlock] = in.stk[(size_t)k * in.cap + j];
+        }
+        const Ray r = load_ray(cur, i);
+        open = !trav4_run<SM>(S, r, 0.0001, node, sp, best, bend, bp, stk, budget);
+        if (!open) W.hit[i] = make_double2(__longlong_as_double((long long)(bp >= 0 ? S.lprim[bp] : bp)), bend);
+    }
+    if (budget < 0) return;  // the last phase suspends nothing
+    const uint32_t slot = block_slot1(open, out_cnt);
+    if (open) {
+        out.idx[slot] = i; out.node[slot] = node; out.sp[slot] = sp; out.bp[slot] = bp;
+        out.best[slot] = best; out.bend[slot] = bend;
+        for (int k = 0; k < sp; ++k) out.stk[(size_t)k * out.cap + slot] = stk.lds[k * kBlock];
     }
 }
 
@@ -1659,6 +1872,17 @@ hipError_t wfs_shade_sm(const SceneRef& s, const WfState& w, const uint32_t* que
     return hipGetLastError();
 }
 #endif  // RS_TU_MODES
+
+#if !defined(RS_TU) || RS_TU == 2  // flat scenes: the phased extend
+hipError_t launch_wf_extend_ph(const SceneRef& s, const WfState& w, uint32_t bounce, const ContSet& in,
+                               const uint32_t* in_cnt, const ContSet& out, uint32_t* out_cnt, int budget, uint32_t blocks,
+                               hipStream_t st) {
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_wf_extend_ph<kSmFlat>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, in, in_cnt, out, out_cnt,
+                       budget);
+    return hipGetLastError();
+}
+#endif
 
 #if defined(RS_TU) && RS_TU >= 0  // this unit's mode
 #define RS_INSTANTIATE_SM(R, NAME, PARAMS, ARGS) template R NAME##_sm<RS_TU> PARAMS;

@@ -28,6 +28,7 @@ def main():
         rec["vmem_rd_per_wave"] = g("SQ_INSTS_VMEM_RD") / waves
         rec["lds_per_wave"] = g("SQ_INSTS_LDS") / waves
         rec["branch_per_wave"] = g("SQ_INSTS_BRANCH") / waves
+        rec["l2_hit"] = g("TCC_HIT_sum") / max(1e-9, g("TCC_HIT_sum") + g("TCC_MISS_sum"))
         rec["lane_util"] = g("SQ_THREAD_CYCLES_VALU") / (64.0 * g("SQ_ACTIVE_INST_VALU"))
         rec["wait_inst_frac"] = g("SQ_WAIT_INST_ANY") / g("SQ_WAVE_CYCLES")
         rec["wait_any_frac"] = g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES")

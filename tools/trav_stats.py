@@ -22,10 +22,11 @@ for name in names:
     lib.rs_debug_trav_stats(out, 1)
     photo.shot(None, world)
     lib.rs_debug_trav_stats(out, 1)
-    nodes, leaves, rays, wmax, lanes, waves = out[:6]
+    nodes, leaves, rays, wmax, lanes, waves, witer = out[:7]
     print(f"{name}: rays {rays} nodes/ray {nodes/max(rays,1):.2f} leaves/ray {leaves/max(rays,1):.2f} "
           f"wave-max nodes {wmax/max(waves,1):.2f} live lanes/wave {lanes/max(waves,1):.1f} "
-          f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f}", flush=True)
+          f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f} "
+          f"leaf passes/wave {witer/max(waves,1):.2f} leaf-pass lane use {leaves/max(64*witer,1):.3f}", flush=True)
     hist = list(out[8:24])
     tot = max(1, sum(hist))
     print("  node steps per ray, 8-wide buckets (%):", " ".join(f"{8*b}:{100*h/tot:.1f}" for b, h in enumerate(hist)), flush=True)

@@ -1,6 +1,7 @@
 # dev: time the bench frame with several library builds (tools/build_variant.sh) in turn; frames are
 # hashed so every variant can be checked bitwise against the first (the in-tree, parity-tested lib).
-# usage: python tools/variant_bench.py [lib.so ...]   (default: all raysnail_amd/lib/var_*.so)
+# usage: python tools/variant_bench.py [--scene=key] [lib.so[:VAR=value,VAR=value] ...]
+#        (default: all raysnail_amd/lib/var_*.so; the VAR=value pairs are that run's environment)
 import glob, hashlib, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r'''
@@ -36,12 +37,17 @@ def main():
     libs = args or [os.path.join(ROOT, "raysnail_amd/lib/libraysnail_hip.so")] + sorted(
         glob.glob(os.path.join(ROOT, "raysnail_amd/lib/var_*.so")))
     expr, spp, depth = SCENES[scene]
-    for lib in libs:
+    for spec in libs:
+        lib, _, envs = spec.partition(":")
+        env = dict(os.environ)
+        for kv in filter(None, envs.split(",")):
+            k, v = kv.split("=", 1)
+            env[k] = v
         code = (CHILD.replace("ROOT", repr(ROOT)).replace("LIB", repr(lib)).replace("SCENE", expr)
                 .replace("SPP", str(spp)).replace("DEPTH", str(depth)))
-        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
         out = r.stdout.strip().splitlines()
-        print(f"{scene} {os.path.basename(lib)}: {out[-1] if out else 'FAILED rc=%d %s' % (r.returncode, r.stderr[-400:])}",
+        print(f"{scene} {os.path.basename(lib)}{':' + envs if envs else ''}: {out[-1] if out else 'FAILED rc=%d %s' % (r.returncode, r.stderr[-400:])}",
               flush=True)
         if r.returncode != 0:
             sys.exit(r.returncode)
