@@ -638,7 +638,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
     s_st_witer[threadIdx.x] = st_witer;
 #endif
     bend_out = bend;
-    return bp >= 0 ? S.lprim[bp] : bp;
+    return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
 template <int SM, class STK>
@@ -1325,6 +1325,9 @@ constexpr int kClsLight = 6;
 // T = 1 and L = 0 implied for the bounce-0 shade kernels). (Writing only the hit and regenerating the
 // camera ray in the bounce-0 shade kernels instead cut 0.27 GB of HBM traffic per launch but made the
 // bench frame slower, 10.20 -> 10.26 ms: the stores are not what bounds this kernel.)
+#ifndef RS_SPH_LEAFQ
+#define RS_SPH_LEAFQ 0  // spheres scenes: queued-leaf traversal (traverse_flat_q) on bounces >= 1 (1) or all (2)
+#endif
 #ifndef RS_EXT_GEN_MIN_WAVES
 #define RS_EXT_GEN_MIN_WAVES 4  // the spheres-mode bounce-0 (camera ray) extend: 144 -> 128 VGPRs, bench frame 7.86 -> 7.63 ms
 #endif
@@ -1336,6 +1339,9 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const StkT<OVF> stk = make_stk<OVF>(S, stk_all);
+#if RS_SPH_LEAFQ
+    __shared__ int leafq[SM == kSmSpheres ? RS_LEAFQ * kBlock : 1];
+#endif
     uint32_t* cnt = W.counts + (size_t)bounce * stride;
     const uint32_t nf = GEN ? 0u : cnt[cix(kCntFront)];
     const uint32_t n = GEN ? n_gen : nf + cnt[cix(kCntBack)];
@@ -1361,7 +1367,12 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
             }
             if (live) {
                 double bend = RS_INF;
+#if RS_SPH_LEAFQ
+                const int bp = (SM == kSmSpheres && (!GEN || RS_SPH_LEAFQ > 1)) ? traverse_flat_q<SM>(S, r, 0.0001, bend, stk, leafq + threadIdx.x)
+                                                  : traverse<SM>(S, r, 0.0001, bend, stk);
+#else
                 const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
+#endif
                 V3 add;
                 bool done = true;
                 if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)

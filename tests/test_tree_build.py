@@ -72,10 +72,11 @@ def test_info_before_commit_is_a_state_error(hip_lib):
 
 
 def test_shading_classes_of_composites():
-    """Host-only commit (no GPU): the material-sorted wavefront's class of each world object is the
-    class of every material its hit records can carry -- quadric.sdl's translated quadric-box
-    intersections (material on the CSG, none on the children) are Lambertian; a CSG whose child
-    brings its own light material next to the CSG's Lambertian one goes to the generic class."""
+    """Host-only commit (no GPU): the material-sorted wavefront's class of a leaf object is its
+    material's; composite objects (CSG, TfFacades of CSG) go to the generic class 4 even when every
+    record they can produce is one class (quadric.sdl's translated quadric-box intersections), so
+    the class queues keep CSG hits apart from leaf hits (rs_host.cpp RS_COMPOSITE_CLASS4); a CSG
+    whose child brings its own light material is class 4 either way."""
     import sys, os
     sys.path.insert(0, os.path.dirname(__file__))
     from raysnail_amd.api import DeviceScene
@@ -83,7 +84,7 @@ def test_shading_classes_of_composites():
     from test_gpu_parity import _emissive_csg_scene
     _, world = scenes.quadric_sdl(64, 64)
     info = DeviceScene(world, devices=[]).info()
-    assert info.scene_mode == 4 and info.class_mask == 0b00001
+    assert info.scene_mode == 4 and info.class_mask == 0b10001
     _, world = _emissive_csg_scene()
     info = DeviceScene(world, devices=[]).info()
     assert info.class_mask == 0b10001
