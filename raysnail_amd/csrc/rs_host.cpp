@@ -175,6 +175,7 @@ struct Replica {
     // wavefront path state (capacity wf_cap paths) + per-chunk queue counters
     void* d_wf = nullptr; size_t wf_cap = 0;
     uint32_t* d_counts = nullptr; size_t counts_cap = 0;
+    size_t counts_clean = 0;  // leading entries of d_counts known to be zero (reset by the last frame's accumulate)
     int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
     // wavefront lanes: independent chunks of a batch in flight together on lane streams (lane 0 =
     // the caller's stream), each with its own path sets and class queues
@@ -589,6 +590,58 @@ int32_t collapse4(const std::vector<HNode>& bn, int32_t code, std::vector<HNode4
     }
     return idx;
 }
+// Reference-order scenes: collapse the reference's binary tree into a 4-wide one whose slots keep the
+// recursion's left-to-right order (an inner slot is replaced IN PLACE by its two children), so a walk
+// of the slots in order, each child's box tested when it is reached, visits the objects in
+// BVH::hit's sequence with the same ranges (bvh.rs:173-192): a skipped intermediate box contains its
+// children's (f32 boxes rounded outward, monotone plane tests), so when it would have failed at range
+// r its first child fails at r too, nothing inside it is visited, the range stays r and its second
+// child fails as well -- whether or not ranges only shrink (Difference back faces).
+int32_t collapse4_inorder(const std::vector<HNode>& bn, int32_t code, std::vector<HNode4>& out, int depth,
+                          int& max_depth) {
+    if (code < 0) return code;
+    max_depth = std::max(max_depth, depth + 1);
+    struct Slot { double lo[3], hi[3]; int32_t c; };
+    std::vector<Slot> slots;
+    auto children = [&](int32_t node, std::vector<Slot>& to, size_t at) {
+        const HNode& n = bn[node];
+        size_t pos = at;
+        for (int k = 0; k < 2; ++k) {
+            if (n.child[k] == INT32_MIN) continue;
+            Slot sl; sl.c = n.child[k];
+            for (int a = 0; a < 3; ++a) { sl.lo[a] = n.lo[k][a]; sl.hi[a] = n.hi[k][a]; }
+            to.insert(to.begin() + pos++, sl);
+        }
+    };
+    children(code, slots, 0);
+    while (slots.size() < 4) {
+        int best = -1; double best_area = -1;
+        for (size_t i = 0; i < slots.size(); ++i) {
+            if (slots[i].c < 0) continue;
+            const double dx = slots[i].hi[0] - slots[i].lo[0], dy = slots[i].hi[1] - slots[i].lo[1], dz = slots[i].hi[2] - slots[i].lo[2];
+            const double ar = dx * dy + dy * dz + dz * dx;
+            if (ar > best_area) { best_area = ar; best = (int)i; }
+        }
+        if (best < 0) break;
+        const int32_t c = slots[best].c;
+        if ((int)slots.size() - 1 + (bn[c].child[0] != INT32_MIN) + (bn[c].child[1] != INT32_MIN) > 4) break;
+        slots.erase(slots.begin() + best);
+        children(c, slots, (size_t)best);
+    }
+    const int32_t idx = (int32_t)out.size();
+    out.emplace_back();
+    int32_t kids[4];
+    for (int k = 0; k < 4; ++k) kids[k] = (size_t)k < slots.size() ? collapse4_inorder(bn, slots[k].c, out, depth + 1, max_depth) : INT32_MIN;
+    HNode4& o = out[idx];
+    for (int k = 0; k < 4; ++k) {
+        o.child[k] = kids[k];
+        for (int q = 0; q < 3; ++q) {
+            o.lo[k][q] = (size_t)k < slots.size() ? slots[k].lo[q] : INFINITY;
+            o.hi[k][q] = (size_t)k < slots.size() ? slots[k].hi[q] : -INFINITY;
+        }
+    }
+    return idx;
+}
 // Exact worst-case stack depth of traverse() (rs_kernels.hip) over a tree: the most entries any
 // root-to-node path can leave on the stack.
 //  4-wide near-first: a node pushes (inner children hit) - 1 <= (inner children) - 1 entries;
@@ -600,6 +653,16 @@ int stack_need4(const std::vector<HNode4>& n4, int32_t code) {
         if (c >= 0) { ++inner; deepest = std::max(deepest, stack_need4(n4, c)); }
     }
     return std::max(inner - 1, 0) + deepest;
+}
+//  4-wide reference order: the node (with its next slot) when an inner child before slot 3 is entered;
+int stack_need4_ref(const std::vector<HNode4>& n4, int32_t code) {
+    if (code < 0) return 0;
+    int need = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int32_t c = n4[code].child[k];
+        if (c >= 0) need = std::max(need, (k < 3 ? 1 : 0) + stack_need4_ref(n4, c));
+    }
+    return need;
 }
 //  binary near-first: one entry (the farther child) when both children are inner nodes;
 int stack_need2(const std::vector<HNode>& bn, int32_t code) {
@@ -947,6 +1010,27 @@ void build(rs_scene* s) {
             s->tree_depth = depth4;
             s->n_nodes = n4.size();
             s->stack_need = stack_need4(n4, r4);
+        }
+    }
+#ifndef RS_REF4
+#define RS_REF4 1  // reference-order scenes on the in-order 4-wide tree (collapse4_inorder)
+#endif
+    // (nest-0 / nest-2 modes; the generic mode's out-of-line traversal measured 3 % slower on it: X2)
+    if (RS_REF4 && s->ref_order && (s->scene_mode == kSmNest0 || s->scene_mode == kSmNest2) && root >= 0 &&
+        !std::getenv("RS_NO_BVH4")) {
+        std::vector<HNode4> n4;
+        int depth4 = 0;
+        const int32_t r4 = collapse4_inorder(B.nodes, root, n4, 0, depth4);
+        if (r4 >= 0) {
+            if (n4.size() * sizeof(DNode4) > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "scene too large: 4-wide tree over 4 GiB");
+            std::vector<DNode4> dn4;
+            for (const HNode4& h : n4) dn4.push_back(to_device4(h));
+            stage(s, d.nodes4, dn4);
+            d.root4 = r4;
+            s->tree_arity = 4;
+            s->tree_depth = depth4;
+            s->n_nodes = n4.size();
+            s->stack_need = stack_need4_ref(n4, r4);
         }
     }
     d.stack_need = s->stack_need;
@@ -1319,7 +1403,9 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     if (wavefront && N > 0) {
         carve_wf(R, chunk, lanes);
         const size_t nc = (size_t)n_chunks_total * (st->depth + 1) * cstride + n_cc;
+        uint32_t* const prev_counts = R.d_counts;
         ensure(R.d_counts, R.counts_cap, nc);
+        if (R.d_counts != prev_counts) R.counts_clean = 0;
         if (phased) carve_cont(R, R.wf_cap, lanes, s->stack_need);
         for (uint32_t l = 1; l < lanes; ++l) {
             if (!R.lane_stream[l]) HIP_OK(hipStreamCreateWithFlags(&R.lane_stream[l], hipStreamNonBlocking));
@@ -1359,10 +1445,16 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     auto kev = [&](size_t i) -> hipEvent_t { return timed ? P.kev[i] : nullptr; };
     auto record = [&](size_t i) { if (timed) HIP_OK(hipEventRecord(P.ev[i], stream)); };
     const SceneRef ds = R.ref();
-    HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
-    if (wavefront && N > 0)
-        HIP_OK(hipMemsetAsync(R.d_counts, 0, (cc_base + n_cc) * sizeof(uint32_t), stream));
+    // the megakernel's segment counters; the wavefront's queue counters start zeroed -- either the
+    // previous frame's last accumulate reset them (counts_clean) or a memset does it here
+    if (!wavefront || timed) HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
+    const size_t n_counts = wavefront && N > 0 ? cc_base + n_cc : 0;
+    if (n_counts > R.counts_clean) HIP_OK(hipMemsetAsync(R.d_counts, 0, n_counts * sizeof(uint32_t), stream));
+    R.counts_clean = 0;
     if (N == 0) HIP_OK(hipMemsetAsync(R.d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
+    FinalParams fp;
+    fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rows.begin; fp.row_step = rows.step; fp.n_samples = N;
+    fp.gamma = st->gamma; fp.mask = d_mask;
     uint32_t bi = 0;
     size_t ki = 0;
     uint64_t chunk_i = 0;
@@ -1466,12 +1558,14 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
             }
         }
         record(2 * bi + 1);
-        HIP_OK(launch_accumulate(R.d_rad, R.d_acc, n_pix, nb, s0 == 0, stream));
+        // the last batch's accumulate finishes the frame (into_color) and, when no statistics read
+        // the queue counters afterwards, zeroes them for the next frame (no memset launch there)
+        const bool last = s0 + spb >= N;
+        const size_t nz = (last && !timed) ? n_counts : 0;
+        HIP_OK(launch_accumulate(R.d_rad, R.d_acc, n_pix, nb, s0 == 0, last, fp, d_out, R.d_counts, (uint32_t)nz, stream));
+        if (last) R.counts_clean = nz;
     }
-    FinalParams fp;
-    fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rows.begin; fp.row_step = rows.step; fp.n_samples = N;
-    fp.gamma = st->gamma; fp.mask = d_mask;
-    HIP_OK(launch_finalize(R.d_acc, d_out, fp, stream));
+    if (N == 0) HIP_OK(launch_finalize(R.d_acc, d_out, fp, stream));
     if (!R.busy) HIP_OK(hipEventCreateWithFlags(&R.busy, hipEventDisableTiming));
     HIP_OK(hipEventRecord(R.busy, stream));
     R.busy_stream = stream;

@@ -172,8 +172,11 @@ hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, u
                         unsigned long long* count, hipStream_t st);
 hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
                             hipStream_t st);
-// acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic).
+// acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic); the last
+// batch writes into_color of the sum into the frame instead (k_finalize's arithmetic, one launch less)
+// and zeroes zero[0, n_zero) (the frame's queue counters) for the next frame.
 hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch, int first_batch,
+                             int last_batch, const FinalParams& p, float* out_rgba, uint32_t* zero, uint32_t n_zero,
                              hipStream_t st);
 // into_color + RGBA f32 store into the full frame.
 hipError_t launch_finalize(const double* acc, float* out_rgba, const FinalParams& p, hipStream_t st);

@@ -681,7 +681,43 @@ __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, doub
         test_leaf<SM>(S, ~(code), r, rc, tmin, best, bend, bp);                \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
-    if (S.root4 >= 0) {
+    if ((SM == kSmNest0 || SM == kSmNest2) && S.root4 >= 0 && S.ref_order) {
+        // BVH::hit's recursion order on the in-order 4-wide tree (rs_host.cpp collapse4_inorder): the
+        // slots of a node left to right, each child's box tested when it is reached with the range the
+        // slots before it left behind; entering an inner child pushes (node, next slot).
+        int k = 0;
+        node = S.root4;
+        while (true) {
+            const uint32_t nb = (uint32_t)node * (uint32_t)sizeof(DNode4) + 4u * (uint32_t)k;
+            const int c = gld<int>(S.nodes4, nb + 96u);
+            if (c == INT32_MIN) {  // slots are filled from the left: the node is done
+                if (sp == 0) break;
+                --sp;
+                const int v = stk.get(sp);
+                node = v >> 2; k = v & 3;
+                continue;
+            }
+            const float lo[3] = {gld<float>(S.nodes4, nb), gld<float>(S.nodes4, nb + 16u), gld<float>(S.nodes4, nb + 32u)};
+            const float hi[3] = {gld<float>(S.nodes4, nb + 48u), gld<float>(S.nodes4, nb + 64u), gld<float>(S.nodes4, nb + 80u)};
+            float e;
+            if (slab32(lo, hi, rf, tmin32, best32, e)) {
+                RS_ST_NODE();
+                if (c < 0) {
+                    RS_LEAF(c);
+                } else {
+                    if (k < 3) { stk.put(sp, node * 4 + k + 1); ++sp; }  // come back for the next slot
+                    node = c;
+                    k = 0;
+                    continue;
+                }
+            }
+            if (k < 3) { ++k; continue; }
+            if (sp == 0) break;
+            --sp;
+            const int v = stk.get(sp);
+            node = v >> 2; k = v & 3;
+        }
+    } else if (S.root4 >= 0) {
         // 4-wide near-first (bvh4_step): nearest inner child next, the rest pushed far-to-near
         const RayF4 rq = make_rayf4(rf);
         node = S.root4;
@@ -1611,8 +1647,12 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? 1 : RS_SHADE_ALL_WAVES) vo
 // a frame has few pixels, and a thread per pixel looping over 3 x N dependent loads left the kernel
 // latency-bound (80 us for the N = 8 share of the bench frame).
 __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict__ rad, double* __restrict__ acc, uint32_t n_pix,
-                                                      uint32_t n_samp, int first) {
+                                                      uint32_t n_samp, int first, int last, FinalParams P,
+                                                      float* __restrict__ out, uint32_t* __restrict__ zero, uint32_t n_zero) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    // the frame's queue counters, read by no kernel after this one: reset for the next frame
+    // (rs_host.cpp counts_clean; the host passes n_zero = 0 when it still reads them)
+    for (uint64_t z = t; z < n_zero; z += (uint64_t)gridDim.x * kBlock) zero[z] = 0u;
     if (t >= 3ull * n_pix) return;
     const uint32_t c = (uint32_t)(t / n_pix), p = (uint32_t)(t - (uint64_t)c * n_pix);
     const uint64_t n_items = (uint64_t)n_pix * n_samp;
@@ -1627,7 +1667,19 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict_
         for (int k = 0; k < 16; ++k) a = a + v[k];
     }
     for (; s < n_samp; ++s) a = a + rc[(uint64_t)s * n_pix];
-    acc[(uint64_t)c * n_pix + p] = a;
+    if (!last) {
+        acc[(uint64_t)c * n_pix + p] = a;
+        return;
+    }
+    // the last batch: into_color of this channel (k_finalize's arithmetic) straight into the frame
+    const uint32_t x = p % P.width;
+    const uint32_t y = P.row_begin + (p / P.width) * P.row_step;
+    const uint64_t pix = (uint64_t)y * P.width + x;
+    const bool masked = P.mask && !P.mask[pix];
+    double v = a / (double)P.n_samples;
+    if (P.gamma) v = sqrt(v);
+    out[pix * 4 + c] = masked ? 0.0f : (float)v;
+    if (c == 0) out[pix * 4 + 3] = masked ? 0.0f : 1.0f;
 }
 #endif  // RS_TU_COMMON
 
@@ -1998,10 +2050,12 @@ hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, d
 }
 
 hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch, int first_batch,
+                             int last_batch, const FinalParams& p, float* out_rgba, uint32_t* zero, uint32_t n_zero,
                              hipStream_t st) {
     const uint32_t blocks = (uint32_t)((3ull * n_pix + kBlock - 1) / kBlock);
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kBlock), 0, st, rad, acc, n_pix, n_samp_batch, first_batch);
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kBlock), 0, st, rad, acc, n_pix, n_samp_batch, first_batch,
+                       last_batch, p, out_rgba, zero, n_zero);
     return hipGetLastError();
 }
 

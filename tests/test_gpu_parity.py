@@ -66,7 +66,36 @@ SCENES = {
     "materials": lambda: scenes.materials_scene(96, 64),
     "cornell_smoke": lambda: scenes.cornell_smoke(48, 48),
     "all_feature": lambda: scenes.all_feature_scene(48, 48),
+    "box_field": lambda: _box_field(64, 48),
 }
+
+
+def _box_field(w, h, n=400):
+    """A reference-order scene with a deep tree: n random boxes, a translated quadric-box intersection
+    and a Difference (non-monotone objects), a sphere light -- the in-order 4-wide tree's walk
+    (collapse4_inorder) against the oracle's recursive BVH::hit."""
+    from raysnail_amd.api import (Box, CameraBuilder, Color, Difference, DiffuseLight, Gradient, HittableList,
+                                  Intersection, Lambertian, Metal, Point3, Sphere, World)
+    C32 = Color
+    rng = np.random.default_rng(3)
+    hl = HittableList()
+    for i in range(n):
+        c = rng.uniform(-6, 6, 3) * np.array([1.0, 0.3, 1.0])
+        e = rng.uniform(0.05, 0.6, 3)
+        mat = Lambertian(C32(*rng.uniform(0.1, 0.9, 3))) if i % 3 else Metal(C32(0.8, 0.8, 0.8))
+        hl.add(Box(tuple(c - e), tuple(c + e), mat))
+    q = scenes._quad((1.0, -1.0, 1.0), (0, 0, 0), (0, 0, 0), 0.0)
+    hl.add(scenes._translated(Intersection(q, Box((-1.0, -1.0, -1.0), (1.0, 1.0, 1.0), None),
+                                           Lambertian(C32(0.7, 0.8, 0.5))), (0.5, 1.5, 0.5)))
+    hl.add(Difference(Box((-2.0, 2.0, -2.0), (-1.0, 3.0, -1.0), Lambertian(C32(0.4, 0.6, 0.8))),
+                      Sphere((-1.5, 2.5, -1.5), 0.6, Lambertian(C32(0.9, 0.2, 0.2))), None))
+    lights = HittableList()
+    lamp = Sphere((0.0, 30.0, 10.0), 4.0, DiffuseLight(C32(1.0, 0.9, 0.8)).multiplier(4.0))
+    lights.add(lamp)
+    hl.add(lamp)
+    cam = CameraBuilder().look_from(Point3(9.0, 4.0, 11.0)).look_at(Point3(0.0, 0.0, 0.0)).fov(50.0) \
+        .width(w).height(h).build()
+    return cam, World(hl, lights, Gradient(C32(0.3, 0.4, 0.5), C32(0.7, 0.89, 1.0)), (0.0, 0.0))
 
 
 @pytest.mark.parametrize("mode", [A.RS_MODE_MEGAKERNEL, A.RS_MODE_WAVEFRONT])

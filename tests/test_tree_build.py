@@ -55,10 +55,14 @@ def test_skewed_deep_scene_commits():
     assert i.tree_arity == 4 and i.stack_need >= 1
 
 
-def test_reference_order_scene_reports_binary_tree():
+def test_reference_order_scene_reports_inorder_4wide_tree():
+    """Reference-order scenes (Box / Quadric / CSG) run on the in-order 4-wide collapse of the
+    reference's tree (rs_host.cpp collapse4_inorder): one stack entry per entered inner child before
+    slot 3, so the worst-case stack is at most the 4-wide depth."""
     _, world = scenes.quadric_sdl(32, 32)
     i = _info(world)
-    assert i.tree_arity == 2 and i.ref_order == 1
+    assert i.tree_arity == 4 and i.ref_order == 1
+    assert 1 <= i.stack_need <= i.tree_depth
 
 
 def test_info_before_commit_is_a_state_error(hip_lib):
