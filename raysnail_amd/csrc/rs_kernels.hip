@@ -647,11 +647,16 @@ template <int SM, class STK>
 __device__ __noinline__ int traverse_call(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     return traverse_body<SM>(S, r, tmin, bend_out, stk);
 }
-// inlined into the kernels of every scene mode but the generic one (a real call makes the kernel
-// keep its live registers in scratch across it: the nest-2 extend spilled 1.2 KB per lane)
+// inlined into the kernels of every scene mode (a real call makes the kernel keep its live registers
+// in scratch across it: the nest-2 extend spilled 1.2 KB per lane); RS_GENERIC_CALL=1 keeps it a call
+// in the generic (rich) mode, measured slower there in round 3 (X1 400x400x16 54.7 vs 51.9 ms, X2
+// 300x300x64 36.9 vs 36.0 ms, bit-identical: profiles/r3/ab/generic_inline_*.txt)
 template <int SM, class STK>
 __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
-    if constexpr (SM == kSmGeneric) return traverse_call<SM>(S, r, tmin, bend_out, stk);
+#ifndef RS_GENERIC_CALL
+#define RS_GENERIC_CALL 0
+#endif
+    if constexpr (SM == kSmGeneric && RS_GENERIC_CALL) return traverse_call<SM>(S, r, tmin, bend_out, stk);
     else return traverse_body<SM>(S, r, tmin, bend_out, stk);
 }
 template <int SM, class STK>
@@ -681,7 +686,9 @@ __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, doub
         test_leaf<SM>(S, ~(code), r, rc, tmin, best, bend, bp);                \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
-    if ((SM == kSmNest0 || SM == kSmNest2) && S.root4 >= 0 && S.ref_order) {
+    // (the generic mode carries it too: its kernels include the World::hit probe, k_probe_hit, which
+    // serves every scene mode's trees)
+    if ((SM == kSmNest0 || SM == kSmNest2 || SM == kSmGeneric) && S.root4 >= 0 && S.ref_order) {
         // BVH::hit's recursion order on the in-order 4-wide tree (rs_host.cpp collapse4_inorder): the
         // slots of a node left to right, each child's box tested when it is reached with the range the
         // slots before it left behind; entering an inner child pushes (node, next slot).
@@ -717,7 +724,7 @@ __device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, doub
             const int v = stk.get(sp);
             node = v >> 2; k = v & 3;
         }
-    } else if (S.root4 >= 0) {
+    } else if (S.root4 >= 0 && !S.ref_order) {
         // 4-wide near-first (bvh4_step): nearest inner child next, the rest pushed far-to-near
         const RayF4 rq = make_rayf4(rf);
         node = S.root4;
