@@ -352,6 +352,40 @@ def test_lanes_and_async_bit_identical(gpu, monkeypatch, name):
         assert np.array_equal(f, ref)
 
 
+def test_queue_counter_reset_across_frames(gpu):
+    """The last accumulate of an asynchronous frame zeroes the frame's queue counters for the next
+    one (no memset, rs_host.cpp counts_clean); frames with statistics keep them for the readback and
+    the next frame zeroes them itself. Mixed sequences -- asynchronous, with statistics, a row share
+    (fewer counters), the full frame again, a longer depth (more counters) -- must each give the
+    oracle's frame and, with statistics, its world.hit count."""
+    import torch
+    cam, world = scenes.rtow_13_1(96, 60)[:2]
+    ds = world.device_scene()
+    s = torch.cuda.current_stream().cuda_stream
+    out = torch.zeros((60, 96, 4), dtype=torch.float32, device="cuda")
+    orc = _oracle(world)
+    cases = {}
+    for key, photo in (("d8", cam.take_photo().samples(16).depth(8).seed(5)),
+                       ("d8_share", cam.take_photo().samples(16).depth(8).seed(5).rows(0, 0, 4)),
+                       ("d20", cam.take_photo().samples(16).depth(20).seed(5))):
+        st = photo.settings()
+        ref, rstats = orc.render(cam.desc, st)
+        cases[key] = (st, ref, rstats)
+    for key, with_stats in (("d8", False), ("d8", False), ("d8", True), ("d8_share", False), ("d8", False),
+                            ("d20", False), ("d20", True), ("d8", False), ("d8_share", True), ("d8", False)):
+        st, ref, rstats = cases[key]
+        out.zero_()
+        stats = ds.render_device(cam.desc, st, out.data_ptr(), s, stats=with_stats)
+        torch.cuda.synchronize()
+        img = out.cpu().numpy()
+        if key == "d8_share":
+            assert np.array_equal(img[0::4], ref[0::4]), key
+        else:
+            assert np.array_equal(img, ref), key
+        if with_stats:
+            assert stats.segments == rstats.segments, (key, stats.segments, rstats.segments)
+
+
 def _emissive_csg_scene(w=80, h=60):
     """Composite prims whose records carry a DiffuseLight (an Intersection with the light on the
     CSG, a TfFacade of it) next to Lambertian CSG: the material-sorted wavefront must emit for them
