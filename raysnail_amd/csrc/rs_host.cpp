@@ -416,7 +416,7 @@ struct Builder {
     LeafSink* leaves = nullptr;
     int max_leaf = 1;   // objects per leaf
     int sah_depth = 48; // SAH splits above this depth, median splits below (bounds the depth)
-    static constexpr size_t kSweepMax = 1024;
+    size_t kSweepMax = 1024;  // full-sweep SAH up to this range size, binned above (RS_SAH_SWEEP overrides)
     static constexpr int kBins = 32;
     int max_depth = 0;
     static double area(const Box3& b) {
@@ -877,6 +877,7 @@ void build(rs_scene* s) {
     // 100 % slower -- a wave serialises its lanes' longer leaf loops)
     B.max_leaf = 1;
     if (const char* ev = std::getenv("RS_SAH_DEPTH")) B.sah_depth = std::max(0, std::atoi(ev));
+    if (const char* ev = std::getenv("RS_SAH_SWEEP")) B.kSweepMax = (size_t)std::max(2LL, std::atoll(ev));
     int32_t root = -1;
     if (!items.empty()) {
         Box3 rb;
