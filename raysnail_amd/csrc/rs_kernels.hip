@@ -2,12 +2,15 @@
 //
 //   k_path_mega   painter.rs:154-187 (render_pixel, one sample) -> camera.rs:77-85 (Camera::ray)
 //                 -> camera.rs:156-255 (ray_color, iterated) with BVH traversal (bvh.rs:173-192)
-//   k_accumulate  painter.rs:167-179 color_vec sum, in sample order
-//   k_finalize    vec3.rs:227-240 into_color (/N, sqrt gamma, f32, alpha 1) + painter.rs:204-210 mask
+//   k_wfs_extend / k_wfs_shade_all / k_wf_*   the wavefront form of the same recursion
+//   k_accumulate  painter.rs:167-179 color_vec sum, in sample order; its last batch also does
+//                 vec3.rs:227-240 into_color (/N, sqrt gamma, f32, alpha 1) + painter.rs:204-210 mask
+//   k_finalize    into_color alone (frames without samples)
 //
 // Build with -ffp-contract=off (see Makefile): the f64 arithmetic mirrors the reference's
-// operation order, so the only differences from the CPU oracle are ocml vs glibc ulps in
-// sin/cos/pow (documented tolerance in DESIGN.md).
+// operation order (explicit fma() only where raysnail calls mul_add); sin/cos/pow are the
+// correctly rounded ones of include/rs_crmath.h on both sides, so GPU frames equal the CPU
+// oracle's bit for bit.
 #include <cstdlib>
 
 #include <hip/hip_ext.h>
