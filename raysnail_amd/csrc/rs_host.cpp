@@ -1617,8 +1617,11 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
                 if (cstride_f > 1)
                     for (int k = 0; k < kWfsClasses; ++k)
                         for (uint32_t g = 0; g < kQSub; ++g) cb += q[cix(1 + k, g)];
-                if (b == 0) { seg0 += q[0]; cont0 += cb; }
-                seg += q[0];
+                uint64_t live = q[0];  // bounces >= 1; bounce 0 counts on kStatLines lines
+                if (cstride_f > 1)
+                    for (uint32_t k = 0; k < kStatLines; ++k) live += q[cix(kCntStat0 + (int)k)];
+                if (b == 0) { seg0 += live; cont0 += cb; }
+                seg += live;
                 cont += cb;
             }
     }

@@ -137,7 +137,11 @@ constexpr uint32_t kCntPad = RS_CNT_PAD;
 #define RS_QSUB 1  // measured: 4, 8, 16 sub-queues are slower (bench frame 9.06 -> 9.18, 9.25, 9.39 ms)
 #endif
 constexpr uint32_t kQSub = RS_QSUB;
-constexpr uint32_t kWfsStride = 8 * kQSub * kCntPad;
+// slots per bounce: 0 live paths, 1-5 class queues, 6 / 7 front / back runs of the next set,
+// 8 .. 8 + kStatLines - 1 the bounce-0 live-sample count spread over lines (summed by the host)
+constexpr int kCntStat0 = 8;
+constexpr uint32_t kStatLines = 8;
+constexpr uint32_t kWfsStride = (8 + kStatLines) * kQSub * kCntPad;
 // word index of counter `slot` (0 live, 1 + k class k, kCntFront, kCntBack), sub-counter g, in a bounce's block
 __host__ __device__ constexpr uint32_t cix(int slot, uint32_t g = 0) { return ((uint32_t)slot * kQSub + g) * kCntPad; }
 __host__ __device__ constexpr uint32_t qsub_cap(uint32_t cap) {

@@ -1474,7 +1474,10 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
         const uint32_t g = (base / kBlock) % kQSub;
         uint32_t* const cs[kClasses] = {&cnt[cix(1, g)], &cnt[cix(2, g)], &cnt[cix(3, g)], &cnt[cix(4, g)], &cnt[cix(5, g)]};
         // bounce 0 also counts its live camera samples (segments, stats) in the same block reduction
-        const uint32_t slot = block_slot<kClasses>(cls, cs, live, GEN ? &cnt[cix(0)] : nullptr);
+        // (the live-sample count goes to one of kStatLines counters on their own lines, by block: a
+        // single word takes ~88 atomics/us, and one per block of a 25.6 M-sample launch kept the
+        // bounce-0 kernel near that ceiling -- 1.14 ms for an empty launch, 0.10 ms spread)
+        const uint32_t slot = block_slot<kClasses>(cls, cs, live, GEN ? &cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))] : nullptr);
         if (cls >= 0) queues[cls][g * W.qsub + slot] = i;
     }
 }
