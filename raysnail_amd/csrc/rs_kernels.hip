@@ -1215,6 +1215,13 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
         live = camera_sample(C, P, item, r, rng);
         if (!live) { rad[item] = 0.0; rad[P.n_items + item] = 0.0; rad[2 * P.n_items + item] = 0.0; }
     }
+    if (!P.mask && P.depth > 0) {
+        // no pixel mask: every camera sample is live, so record i is thread i's (no compaction, and
+        // no returning atomic per block on one word -- ~88/us, which bounded this kernel)
+        if (i == 0) W.counts[0] = n;
+        if (live) store_path(W.set[0], i, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
+        return;
+    }
     const uint32_t slot = block_slot1(live, &W.counts[0]);
     if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
 }
