@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 4
+#define RS_ABI_VERSION 5
 
 /* ---- status codes ---- */
 #define RS_OK             0
@@ -273,10 +273,24 @@ int rs_scene_commit(rs_scene* s);
  * works, rendering returns RS_E_STATE. */
 int rs_scene_commit_devices(rs_scene* s, const int* devices, int n);
 int rs_scene_get_info(const rs_scene* s, rs_scene_info* out);
-/* wavefront lanes for the scene's later renders: the chunks of a batch run round-robin on this many
- * concurrent streams (1 .. 4; default 2, or RS_LANES at rs_scene_create). No reference counterpart
- * (a scheduling knob like Painter::threads, painter.rs:318-325); frames are bitwise the same. */
+/* wavefront lanes for the scene's later renders (1 .. 4): concurrent streams within one frame. The
+ * bounce-synchronous wavefront (flat / mesh and rich scenes) deals the chunks of a batch to them
+ * round robin (default 2); the streaming wavefront (spheres / box / CSG scenes) deals whole sample
+ * batches to lanes, each with its own pool of paths (default 1). No reference counterpart (a
+ * scheduling knob like Painter::threads, painter.rs:318-325); frames are bitwise the same. */
 int rs_scene_set_lanes(rs_scene* s, uint32_t lanes);
+/* frames in flight per device (1 .. 4; default 2): consecutive asynchronous frames are dealt to this
+ * many frame slots, each with its own streams and buffers, and a frame waits only for the previous
+ * frame of its slot -- the next frame's first paths are traced while the previous frame's last paths
+ * drain. Output and stream semantics are unchanged: a frame's result is written on the call's stream,
+ * in call order; a frame with a mask (or statistics) also waits for the work queued on its stream
+ * before the call. No reference counterpart (painter.rs renders one frame at a time). */
+int rs_scene_set_frames_in_flight(rs_scene* s, uint32_t frames);
+/* workspace sizes (0 = keep): camera samples per radiance batch buffer (default 32 Mi, whole sample
+ * planes are used) and paths per path set (default 64 Mi: the bound of the streaming wavefront's pool
+ * -- camera samples injected per iteration times the iterations a path can span -- and the chunk of
+ * the bounce-synchronous wavefront). Scheduling only: frames are bitwise the same for any value. */
+int rs_scene_set_workspace(rs_scene* s, uint64_t max_batch_items, uint64_t pool_paths);
 
 /* ---- render ---- */
 /* host output: out_rgba = W*H*4 floats; mask = W*H bytes or NULL (all pixels) */

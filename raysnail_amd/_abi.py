@@ -136,6 +136,7 @@ SCENE_SIGNATURES = {
 }
 
 _LIB = None
+ABI_VERSION = 5  # include/raysnail_hip.h RS_ABI_VERSION
 
 
 def lib_path() -> str:
@@ -184,10 +185,13 @@ def load() -> C.CDLL:
     lib.rs_scene_get_info.argtypes = [VP, C.POINTER(rs_scene_info)]
     lib.rs_scene_commit_devices.argtypes = [VP, C.POINTER(C.c_int), C.c_int]
     lib.rs_scene_set_lanes.argtypes = [VP, C.c_uint32]
-    for fn in ("rs_probe_world_hit", "rs_scene_get_info", "rs_scene_set_lanes", "rs_scene_commit_devices", "rs_scene_create", "rs_scene_destroy", "rs_scene_commit", "rs_render", "rs_render_device",
-               "rs_device_count"):
+    lib.rs_scene_set_frames_in_flight.argtypes = [VP, C.c_uint32]
+    lib.rs_scene_set_workspace.argtypes = [VP, C.c_uint64, C.c_uint64]
+    for fn in ("rs_probe_world_hit", "rs_scene_get_info", "rs_scene_set_lanes", "rs_scene_set_frames_in_flight",
+               "rs_scene_set_workspace", "rs_scene_commit_devices", "rs_scene_create", "rs_scene_destroy",
+               "rs_scene_commit", "rs_render", "rs_render_device", "rs_device_count"):
         getattr(lib, fn).restype = C.c_int
-    if lib.rs_abi_version() != 4:
+    if lib.rs_abi_version() != ABI_VERSION:
         raise RuntimeError("libraysnail_hip.so ABI mismatch")
     _LIB = lib
     return lib
@@ -198,6 +202,7 @@ EXPORTED_SYMBOLS = [
     "rs_abi_version", "rs_last_error", "rs_device_count", "rs_stream_key", "rs_medium_uniform", "rs_scene_create",
     "rs_scene_destroy", "rs_perlin", "rs_image", "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
     "rs_difference", "rs_transformed", "rs_constant_medium", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
-    "rs_scene_commit", "rs_scene_commit_devices", "rs_scene_get_info", "rs_scene_set_lanes", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
+    "rs_scene_commit", "rs_scene_commit_devices", "rs_scene_get_info", "rs_scene_set_lanes",
+    "rs_scene_set_frames_in_flight", "rs_scene_set_workspace", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
     "rs_probe_world_hit", "rs_probe_samples",
 ]

@@ -549,8 +549,16 @@ class DeviceScene:
         return inf
 
     def set_lanes(self, lanes: int) -> None:
-        """Wavefront lanes (concurrent chunk streams) for later renders (rs_scene_set_lanes)."""
+        """Chunk lanes of the bounce-synchronous wavefront for later renders (rs_scene_set_lanes)."""
         _check(self.lib, self.lib.rs_scene_set_lanes(self.handle, lanes), "rs_")
+
+    def set_frames_in_flight(self, frames: int) -> None:
+        """Frame slots per device: asynchronous frames overlap (rs_scene_set_frames_in_flight)."""
+        _check(self.lib, self.lib.rs_scene_set_frames_in_flight(self.handle, frames), "rs_")
+
+    def set_workspace(self, max_batch_items: int = 0, pool_paths: int = 0) -> None:
+        """Radiance batch size and path-set capacity, 0 = keep (rs_scene_set_workspace); scheduling only."""
+        _check(self.lib, self.lib.rs_scene_set_workspace(self.handle, max_batch_items, pool_paths), "rs_")
 
     def render(self, cam: A.rs_camera_desc, st: A.rs_render_settings, mask: Optional[np.ndarray] = None,
                out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, A.rs_render_stats]:

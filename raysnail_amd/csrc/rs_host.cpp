@@ -159,47 +159,80 @@ struct HostScene {
     std::vector<Blob> blobs;
 };
 
-// One device the scene is committed to: its copy of the scene arrays and its render workspace
-// (grown on demand). A device may appear more than once in rs_scene_commit_devices (virtual
-// devices, e.g. for tests): every replica owns its own stream and buffers.
-struct Replica {
-    int device = 0;
-    hipStream_t stream = nullptr;           // the replica's own stream (multi-device renders)
-    DScene ds{};
-    std::vector<void*> dev;                 // scene allocations
+// One frame in flight on a replica: its streams and the render workspace it owns (grown on demand).
+// Frames are dealt to a replica's slots round robin; a frame waits only for the previous frame of
+// ITS slot (free_ev, recorded after the last kernel that reads the slot's buffers), so the next
+// frame's first iterations run while the previous frame's last paths drain.
+struct Slot {
+    hipStream_t lane[kMaxLanes] = {nullptr};   // lane[0]: the slot's stream; 1..: chunk lanes
+    hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {nullptr};
+    hipEvent_t free_ev = nullptr, entry_ev = nullptr;
+    bool free_rec = false;
     double* d_rad = nullptr; size_t rad_cap = 0;
     double* d_acc = nullptr; size_t acc_cap = 0;
-    unsigned long long* d_cnt = nullptr;
-    uint8_t* d_mask = nullptr; size_t mask_cap = 0;
-    float* d_out = nullptr; size_t out_cap = 0;
-    // wavefront path state (capacity wf_cap paths) + per-chunk queue counters
-    void* d_wf = nullptr; size_t wf_cap = 0;
-    uint32_t* d_counts = nullptr; size_t counts_cap = 0;
-    size_t counts_clean = 0;  // leading entries of d_counts known to be zero (reset by the last frame's accumulate)
-    int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
-    // wavefront lanes: independent chunks of a batch in flight together on lane streams (lane 0 =
-    // the caller's stream), each with its own path sets and class queues
-    uint32_t wf_lanes = 0;
+    unsigned long long* d_cnt = nullptr;     // megakernel segment counters (512)
+    uint8_t* d_mask = nullptr; size_t mask_cap = 0;   // replicas > 0: the caller's mask copied over
+    float* d_out = nullptr; size_t out_cap = 0;       // replicas > 0 / rs_render: the frame on this device
+    // wavefront path state (capacity wf_cap paths per set) per lane + queue counters
+    void* d_wf = nullptr; size_t wf_cap = 0; uint32_t wf_lanes = 0;
     uint32_t** d_qptrs[kMaxLanes] = {nullptr};    // per lane: device array of the per-class queues
     uint32_t* qptr[kMaxLanes][kWfsClasses] = {{nullptr}};
     WfState lane_ws[kMaxLanes]{};
-    hipStream_t lane_stream[kMaxLanes] = {nullptr};  // [1..]: created on first use
-    hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {nullptr};
+    uint32_t* d_counts = nullptr; size_t counts_cap = 0;
+    size_t counts_clean = 0;  // leading entries of d_counts known to be zero (reset by the last frame's accumulate)
+    hipStream_t acc_stream = nullptr;         // streaming wavefront: the batches' accumulates
+    std::vector<hipEvent_t> bev;              // per batch: its paths done, its accumulate done
+
+    // wait until nothing in flight uses this slot's buffers
+    void quiesce() {
+        for (uint32_t l = 0; l < kMaxLanes; ++l)
+            if (lane[l]) HIP_OK(hipStreamSynchronize(lane[l]));
+        if (acc_stream) HIP_OK(hipStreamSynchronize(acc_stream));
+        if (free_rec) HIP_OK(hipEventSynchronize(free_ev));
+    }
+    void release() {
+        for (uint32_t l = 0; l < kMaxLanes; ++l)
+            if (lane[l]) (void)hipStreamSynchronize(lane[l]);
+        if (acc_stream) (void)hipStreamSynchronize(acc_stream);
+        if (free_rec) (void)hipEventSynchronize(free_ev);
+        for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts})
+            if (p) (void)hipFree(p);
+        for (uint32_t l = 0; l < kMaxLanes; ++l) {
+            if (lane[l]) (void)hipStreamDestroy(lane[l]);
+            if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
+        }
+        for (hipEvent_t e : {fork_ev, free_ev, entry_ev})
+            if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : bev) (void)hipEventDestroy(e);
+        if (acc_stream) (void)hipStreamDestroy(acc_stream);
+    }
+};
+
+// One device the scene is committed to: its copy of the scene arrays and its frame slots. A device
+// may appear more than once in rs_scene_commit_devices (virtual devices, e.g. for tests): every
+// replica owns its own streams and buffers.
+struct Replica {
+    int device = 0;
+    hipStream_t stream = nullptr;           // the replica's own stream (multi-device renders, rs_render)
+    DScene ds{};
+    std::vector<void*> dev;                 // scene allocations
+    Slot slots[kMaxSlots];
+    uint32_t next_slot = 0;
+    int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
     int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond kStackMax)
-    // phased flat-scene extend: two continuation sets per lane (ping-pong between phases)
-    void* d_cont = nullptr; size_t cont_bytes = 0;
-    ContSet cont[kMaxLanes][2]{};
     DScene* d_ds = nullptr;                 // ds in device memory (what the kernels read)
     DScene uploaded{};                      // the copy last written to d_ds
-    // asynchronous frames (rs_render_device without stats): the end of the last enqueued frame, so a
-    // frame on another stream waits for it before reusing the replica's buffers
-    hipEvent_t busy = nullptr;
-    hipStream_t busy_stream = nullptr;
 
+    // wait until no frame of this replica is in flight (before a shared buffer is replaced)
+    void quiesce() {
+        for (Slot& sl : slots) sl.quiesce();
+        if (stream) HIP_OK(hipStreamSynchronize(stream));
+    }
     // the scene for a launch, with d_ds brought up to date first (it changes only when the
     // stack-overflow array is reallocated)
     SceneRef ref() {
         if (std::memcmp(&uploaded, &ds, sizeof(DScene)) != 0) {
+            quiesce();
             HIP_OK(hipMemcpy(d_ds, &ds, sizeof(DScene), hipMemcpyHostToDevice));
             uploaded = ds;
         }
@@ -209,17 +242,11 @@ struct Replica {
     ~Replica() {
         int prev = -1;
         const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
-        if (busy) (void)hipEventSynchronize(busy);  // an asynchronous frame may still read the scene
+        for (Slot& sl : slots) sl.release();  // an asynchronous frame may still read the scene
+        if (stream) (void)hipStreamSynchronize(stream);
         for (void* p : dev) (void)hipFree(p);
-        for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts,
-                        (void*)d_ovf, (void*)d_ds, d_cont})
+        for (void* p : {(void*)d_ovf, (void*)d_ds})
             if (p) (void)hipFree(p);
-        for (uint32_t l = 1; l < kMaxLanes; ++l) {
-            if (lane_stream[l]) (void)hipStreamDestroy(lane_stream[l]);
-            if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
-        }
-        if (fork_ev) (void)hipEventDestroy(fork_ev);
-        if (busy) (void)hipEventDestroy(busy);
         if (stream) (void)hipStreamDestroy(stream);
         if (switched) (void)hipSetDevice(prev);
     }
@@ -238,14 +265,16 @@ struct rs_scene {
     bool ref_order = false;                 // BVH::hit recursion order needed (non-monotone objects)
     HostScene hs;                           // device layout, built once by commit
     std::vector<std::unique_ptr<Replica>> reps;   // the devices the scene is committed to, in call order
-    uint64_t wf_chunk = 32ull << 20;              // RS_WF_CHUNK overrides
-    uint32_t wf_lanes = RS_LANES;                 // wavefront lanes (concurrent chunk streams); RS_LANES overrides
-    // phased extend of flat scenes (k_wf_extend_ph): node-step budgets of the bounded phases, then one
-    // phase to the end; ph_n = 0 runs the one-pass extend. RS_PHASES="b0,b1,..." overrides ("0": off).
-    int ph_n = RS_PH_N;
-    int ph_budget[kMaxPhases] = {RS_PH_B0, RS_PH_B1, 0, 0};
+    // workspace (rs_scene_set_workspace): camera samples per rad batch buffer; paths per set of the
+    // streaming pool / per chunk of the bounce-synchronous wavefront
+    uint64_t max_items_per_batch = 32ull << 20;
+    uint64_t pool_paths = 64ull << 20;
+    uint32_t inject_div = 1;                      // streaming: inject up to 1/inject_div of a lane per iteration
+    uint32_t wf_lanes = 2;                        // chunk lanes of the bounce-synchronous wavefront (rs_scene_set_lanes)
+    uint32_t stream_lanes = 1;                    // lanes of the streaming wavefront (rs_scene_set_lanes)
+    uint32_t frames_in_flight = 2;                // frame slots per replica (rs_scene_set_frames_in_flight)
+    bool ext_split = false;                       // streaming extend in two launches per iteration in every mode (dev A/B)
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
-    uint64_t max_items_per_batch = 32ull << 20;  // RS_MAX_BATCH_ITEMS overrides (tests)
     int tree_depth = 0;                     // levels of the tree in use
     int tree_arity = 0;                     // 4: 4-wide tree, 2: binary tree, 0: empty world
     int stack_need = 0;                     // exact worst-case traversal stack depth of that tree
@@ -712,7 +741,6 @@ void upload_replica(rs_scene* s, int device) {
         HIP_OK(hipMemcpy(p, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice));
         std::memcpy((char*)&R->ds + b.field_off, &p, sizeof(void*));
     }
-    HIP_OK(hipMalloc((void**)&R->d_cnt, 512 * sizeof(unsigned long long)));
     HIP_OK(hipMalloc((void**)&R->d_ds, sizeof(DScene)));
     std::memset(&R->uploaded, 0xff, sizeof(DScene));  // forces the first upload
     HIP_OK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
@@ -876,8 +904,13 @@ void build(rs_scene* s) {
     // one object per leaf (measured on the C5 mesh: 2, 4 and 8 objects per leaf were 15 %, 45 % and
     // 100 % slower -- a wave serialises its lanes' longer leaf loops)
     B.max_leaf = 1;
+#ifdef RS_DEV_KNOBS
     if (const char* ev = std::getenv("RS_SAH_DEPTH")) B.sah_depth = std::max(0, std::atoi(ev));
     if (const char* ev = std::getenv("RS_SAH_SWEEP")) B.kSweepMax = (size_t)std::max(2LL, std::atoll(ev));
+    const bool no_bvh4 = std::getenv("RS_NO_BVH4") != nullptr;  // the binary trees, for comparison
+#else
+    const bool no_bvh4 = false;
+#endif
     int32_t root = -1;
     if (!items.empty()) {
         Box3 rb;
@@ -967,12 +1000,9 @@ void build(rs_scene* s) {
     // mixes CSG hits (finish_hit through the nested-object code) with leaf hits, and the next
     // extend's waves of rays leaving both, run the union of both paths (C4, quadric.sdl at depth
     // 50: 46.1 ms per 512x512x64 frame with CSG in class 4, 56.7 ms with it Lambertian-class).
-#ifndef RS_COMPOSITE_CLASS4
-#define RS_COMPOSITE_CLASS4 1
-#endif
     auto class_of = [&](uint32_t h) -> int {
         std::vector<int32_t> ms;
-        if (RS_COMPOSITE_CLASS4 && !is_leafish(h)) return 4;
+        if (!is_leafish(h)) return 4;
         if (!rec_mats(h, ms) || ms.empty()) return 4;
         const int c0 = mat_class(ms[0]);
         for (int32_t m : ms)
@@ -996,7 +1026,7 @@ void build(rs_scene* s) {
     if (root >= 0)
         s->stack_need = s->ref_order ? stack_need_ref(B.nodes, root)
                                      : std::max(stack_need_ref(B.nodes, root), stack_need2(B.nodes, root));
-    if (!s->ref_order && root >= 0 && !std::getenv("RS_NO_BVH4")) {
+    if (!s->ref_order && root >= 0 && !no_bvh4) {
         std::vector<HNode4> n4;
         int depth4 = 0;
         const int32_t r4 = collapse4(B.nodes, root, n4, 0, depth4);
@@ -1013,12 +1043,9 @@ void build(rs_scene* s) {
             s->stack_need = stack_need4(n4, r4);
         }
     }
-#ifndef RS_REF4
-#define RS_REF4 1  // reference-order scenes on the in-order 4-wide tree (collapse4_inorder)
-#endif
-    // (nest-0 / nest-2 modes; the generic mode's out-of-line traversal measured 3 % slower on it: X2)
-    if (RS_REF4 && s->ref_order && (s->scene_mode == kSmNest0 || s->scene_mode == kSmNest2) && root >= 0 &&
-        !std::getenv("RS_NO_BVH4")) {
+    // reference-order scenes on the in-order 4-wide tree (collapse4_inorder), nest-0 / nest-2 modes (the
+    // generic mode measured 3 % slower on it: X2)
+    if (s->ref_order && (s->scene_mode == kSmNest0 || s->scene_mode == kSmNest2) && root >= 0 && !no_bvh4) {
         std::vector<HNode4> n4;
         int depth4 = 0;
         const int32_t r4 = collapse4_inorder(B.nodes, root, n4, 0, depth4);
@@ -1049,6 +1076,8 @@ void build(rs_scene* s) {
         std::memset(lsph.data(), 0, lsph.size() * sizeof(DSphere));
         for (size_t h = 0; h < s->objs.size(); ++h)
             if (s->objs[h].kind == PK_SPHERE) lsph[h] = spheres[prims[h].idx];
+        // the kernels address this array with 32-bit byte offsets (rs_kernels.hip ld_sphere)
+        if (lsph.size() * sizeof(DSphere) > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "scene too large: sphere array over 4 GiB");
         stage(s, d.lsph, lsph);
     }
     if (s->scene_mode == kSmFlat) {
@@ -1062,6 +1091,8 @@ void build(rs_scene* s) {
             for (int k = 0; k < 3; ++k) ltri[e].p0[k] = T.p0[k];
             ltri[e].a = T.a; ltri[e].b = T.b; ltri[e].c = T.c; ltri[e].d = T.d; ltri[e].e = T.e; ltri[e].f = T.f;
         }
+        // the kernels address this array with 32-bit byte offsets (rs_kernels.hip ld_ltri): ~53.7 M entries
+        if (ltri.size() * sizeof(LTri) > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "scene too large: leaf triangle array over 4 GiB");
         stage(s, d.ltri, ltri);
     }
     stage(s, d.rects, rects);
@@ -1195,11 +1226,14 @@ uint64_t splitmix64_h(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-template <typename T>
-void ensure(T*& p, size_t& cap, size_t n) {
+// grow a device buffer; `owner` (a slot or a replica) is quiesced first: frames in flight may still
+// use the old one
+template <typename T, class Q>
+void ensure(Q& owner, T*& p, size_t& cap, size_t n) {
     if (n <= cap) return;
-    if (p) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipFree(p)); }  // frames may still be in flight
+    if (p) { owner.quiesce(); HIP_OK(hipFree(p)); }
     p = nullptr;
+    cap = 0;
     HIP_OK(hipMalloc((void**)&p, n * sizeof(T)));
     cap = n;
 }
@@ -1209,77 +1243,46 @@ void ensure(T*& p, size_t& cap, size_t n) {
 void ensure_stack_overflow(const rs_scene* s, Replica& R, uint64_t threads) {
     const int extra = s->stack_need - kStackMax;
     if (extra <= 0) { R.ds.stk_ovf = nullptr; return; }
-    ensure(R.d_ovf, R.ovf_cap, (size_t)extra * threads);
+    ensure(R, R.d_ovf, R.ovf_cap, (size_t)extra * threads);
     R.ds.stk_ovf = R.d_ovf;
 }
 
-// Path state of `lanes` lanes of capacity `cap` paths each (R.lane_ws[l], R.d_qptrs[l], R.qptr[l]).
-void carve_wf(Replica& R, uint64_t cap, uint32_t lanes) {
-    const size_t per_set = 3 * sizeof(D4) + sizeof(uint32_t);
-    const size_t per = 2 * per_set + sizeof(double2);
-    const uint64_t c = std::max<uint64_t>(cap, R.wf_cap);
-    const uint64_t qcap = (uint64_t)kQSub * qsub_cap((uint32_t)c);  // per class queue
-    const size_t lane_bytes = (per * c + kWfsClasses * sizeof(uint32_t) * qcap + 8192 + 255) & ~(size_t)255;
-    const bool fresh = cap > R.wf_cap || lanes > R.wf_lanes;
+// Path state of `lanes` lanes of capacity `cap` paths per set each (L.lane_ws[l], L.d_qptrs[l], L.qptr[l]).
+void carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
+    const size_t per_set = 3 * sizeof(D4) + sizeof(uint2);
+    const size_t per = 2 * per_set + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
+    const uint64_t c = (std::max<uint64_t>(cap, L.wf_cap) + 255) & ~(uint64_t)255;
+    const size_t lane_bytes = (per * c + 16 * 256 + 8192 + 255) & ~(size_t)255;
+    const bool fresh = c > L.wf_cap || lanes > L.wf_lanes;
     if (fresh) {
-        if (R.d_wf) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipFree(R.d_wf)); }
-        R.d_wf = nullptr;
-        R.wf_cap = 0;
-        R.wf_lanes = 0;
-        HIP_OK(hipMalloc(&R.d_wf, lane_bytes * lanes));
-        R.wf_cap = c;
-        R.wf_lanes = lanes;
+        if (L.d_wf) { L.quiesce(); HIP_OK(hipFree(L.d_wf)); }
+        L.d_wf = nullptr;
+        L.wf_cap = 0;
+        L.wf_lanes = 0;
+        HIP_OK(hipMalloc(&L.d_wf, lane_bytes * lanes));
+        L.wf_cap = c;
+        L.wf_lanes = lanes;
     }
+    auto al = [](char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); };
     for (uint32_t l = 0; l < lanes; ++l) {
-        char* p = (char*)R.d_wf + lane_bytes * l;
-        WfState& w = R.lane_ws[l];
+        char* p = (char*)L.d_wf + lane_bytes * l;
+        WfState& w = L.lane_ws[l];
         for (int k = 0; k < 2; ++k) {
             WfSet& t = w.set[k];
             t.ray_o = (D4*)p; p += sizeof(D4) * c;
             t.ray_d = (D4*)p; p += sizeof(D4) * c;
             t.thr = (D4*)p; p += sizeof(D4) * c;
-            t.item = (uint32_t*)p; p += sizeof(uint32_t) * c;
-            p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+            t.tag = (uint2*)p; p = al(p + sizeof(uint2) * c);
         }
         w.hit = (double2*)p; p += sizeof(double2) * c;
         uint32_t* qp[kWfsClasses];
-        for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p += sizeof(uint32_t) * qcap; }
-        p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
-        R.d_qptrs[l] = (uint32_t**)p;
-        if (fresh) HIP_OK(hipMemcpy(R.d_qptrs[l], qp, sizeof(qp), hipMemcpyHostToDevice));
-        for (int k = 0; k < kWfsClasses; ++k) R.qptr[l][k] = qp[k];
+        for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p = al(p + sizeof(uint32_t) * c); }
+        L.d_qptrs[l] = (uint32_t**)p;
+        if (fresh) HIP_OK(hipMemcpy(L.d_qptrs[l], qp, sizeof(qp), hipMemcpyHostToDevice));
+        for (int k = 0; k < kWfsClasses; ++k) L.qptr[l][k] = qp[k];
         w.counts = nullptr;
         w.cap = (uint32_t)c;
-        w.qsub = qsub_cap((uint32_t)c);
     }
-}
-
-// Continuation sets of the phased extend: per lane two sets of `cap` slots with `rows` stack rows.
-void carve_cont(Replica& R, uint64_t cap, uint32_t lanes, int rows) {
-    const size_t per = 4 * sizeof(int32_t) + 2 * sizeof(double) + (size_t)rows * sizeof(int32_t);
-    const size_t set_bytes = (per * cap + 8 * 256 + 255) & ~(size_t)255;
-    const size_t need = set_bytes * 2 * lanes;
-    if (need > R.cont_bytes) {
-        if (R.d_cont) { HIP_OK(hipDeviceSynchronize()); HIP_OK(hipFree(R.d_cont)); }
-        R.d_cont = nullptr;
-        R.cont_bytes = 0;
-        HIP_OK(hipMalloc(&R.d_cont, need));
-        R.cont_bytes = need;
-    }
-    auto al = [](char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); };
-    for (uint32_t l = 0; l < lanes; ++l)
-        for (int k = 0; k < 2; ++k) {
-            char* p = (char*)R.d_cont + set_bytes * (2 * l + k);
-            ContSet& c = R.cont[l][k];
-            c.idx = (uint32_t*)p; p = al(p + sizeof(uint32_t) * cap);
-            c.node = (int32_t*)p; p = al(p + sizeof(int32_t) * cap);
-            c.sp = (int32_t*)p; p = al(p + sizeof(int32_t) * cap);
-            c.bp = (int32_t*)p; p = al(p + sizeof(int32_t) * cap);
-            c.best = (double*)p; p = al(p + sizeof(double) * cap);
-            c.bend = (double*)p; p = al(p + sizeof(double) * cap);
-            c.stk = (int32_t*)p;
-            c.cap = (uint32_t)cap;
-        }
 }
 
 struct DeviceGuard {
@@ -1309,15 +1312,126 @@ RowSet replica_rows(const rs_camera_desc* cam, const rs_render_settings* st, uin
     return r;
 }
 
+// Streaming schedule of a frame. The frame's camera samples form batches of B items
+// (whole sample planes; the last may be shorter), dealt to L lanes round robin: lane l streams batches
+// l, l + L, ... through its own pool on its own stream, injecting Q samples per iteration. Lane-local
+// item j of lane l is item j - m B of its m-th batch. Batch k may be accumulated once the lane's
+// iteration done(k) (its last sample injected + depth - 1) has run; its radiance lives in buffer
+// k % ring of the rad ring, which a batch may take over only after the batch `ring` earlier was
+// accumulated (the lane waits for that accumulate).
+struct LaneSched {
+    std::vector<uint32_t> batch;        // global batch ids, in the lane's order
+    uint64_t total = 0, Q = 0, T_inj = 0, T = 0, cap = 0;
+    uint64_t cnt_off = 0;               // the lane's counter blocks in the frame's counter array (words)
+    uint64_t B = 0, last_nb = 0;        // batch size, size of the lane's last batch
+    uint32_t D = 0;
+    uint64_t nb(uint64_t m) const { return m + 1 == batch.size() ? last_nb : B; }
+    uint64_t first_it(uint64_t m) const { return (m * B) / Q; }
+    uint64_t done_it(uint64_t m) const {
+        const uint64_t end = std::min((m + 1) * B, total);
+        return std::min((end - 1) / Q + (D ? D - 1 : 0), T - 1);
+    }
+    uint32_t n_new(uint64_t t) const { return t < T_inj ? (uint32_t)std::min(Q, total - t * Q) : 0u; }
+};
+struct FrameSched {
+    uint64_t B = 0;
+    uint32_t n_batches = 0, lanes = 1, ring = 1;
+    std::vector<LaneSched> lane;
+    uint64_t n_counts = 0;              // counter words of all lanes
+    uint64_t cap = 0;                   // pool records per set (the largest lane's)
+};
+// The enqueue order of a frame (render_enqueue walks it; make_sched dry-runs it to size the ring):
+// iterations round robin over the lanes; after each, every accumulate whose batches are complete, in
+// batch order. visit(l, t) for an iteration, acc(k) for an accumulate.
+template <class FI, class FA>
+void walk(const FrameSched& f, FI visit, FA acc) {
+    std::vector<uint64_t> t(f.lanes, 0), m_done(f.lanes, 0);
+    std::vector<char> done(f.n_batches, 0);
+    uint32_t next_acc = 0;
+    for (bool any = true; any;) {
+        any = false;
+        for (uint32_t l = 0; l < f.lanes; ++l) {
+            const LaneSched& L = f.lane[l];
+            if (t[l] >= L.T) continue;
+            any = true;
+            visit(l, t[l]);
+            while (m_done[l] < L.batch.size() && L.done_it(m_done[l]) == t[l]) done[L.batch[m_done[l]++]] = 1;
+            ++t[l];
+            while (next_acc < f.n_batches && done[next_acc]) acc(next_acc++);
+        }
+    }
+}
+FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D, uint32_t want_lanes) {
+    FrameSched f;
+    // batches: at most max_items_per_batch items, and at least one per lane
+    uint32_t spb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(N, s->max_items_per_batch / n_pix));
+    spb = std::min(spb, std::max<uint32_t>(1, (N + want_lanes - 1) / want_lanes));
+    f.B = n_pix * spb;
+    f.n_batches = (N + spb - 1) / spb;
+    f.lanes = std::max<uint32_t>(1, std::min(want_lanes, f.n_batches));
+    f.lane.resize(f.lanes);
+    const uint64_t total = n_pix * N;
+    for (uint32_t k = 0; k < f.n_batches; ++k) {
+        LaneSched& L = f.lane[k % f.lanes];
+        L.batch.push_back(k);
+        const uint64_t nb = std::min(f.B, total - (uint64_t)k * f.B);
+        L.total += nb;
+        L.last_nb = nb;
+    }
+    for (LaneSched& L : f.lane) {
+        L.B = f.B;
+        L.D = D;
+        // about 1/inject_div of the lane per iteration, at most a batch; the pool's bound, Q times the
+        // iterations a path can span, must fit pool_paths
+        const uint64_t Dm = std::max<uint32_t>(D, 1);
+        uint64_t q = std::min<uint64_t>(f.B, std::max<uint64_t>(kBlock, (L.total + s->inject_div - 1) / s->inject_div));
+        auto bound = [&](uint64_t qq) { return qq * std::min<uint64_t>(Dm, (L.total + qq - 1) / qq); };
+        if (bound(q) > s->pool_paths) q = std::min<uint64_t>(f.B, std::max<uint64_t>(kBlock, s->pool_paths / Dm));
+        L.Q = q;
+        L.T_inj = (L.total + q - 1) / q;
+        L.T = L.T_inj + (D ? D - 1 : 0);
+        L.cap = bound(q);
+        L.cnt_off = f.n_counts;
+        f.n_counts += (L.T + 1) * kWfsStride;
+        f.cap = std::max(f.cap, L.cap);
+    }
+    // ring: the most batches ever begun and not yet accumulated in the enqueue order
+    std::vector<uint64_t> start(f.n_batches, UINT64_MAX), acc_at(f.n_batches, 0);
+    uint64_t step = 0;
+    walk(f, [&](uint32_t l, uint64_t t) {
+             const LaneSched& L = f.lane[l];
+             for (uint64_t m = 0; m < L.batch.size(); ++m)
+                 if (L.first_it(m) == t && start[L.batch[m]] == UINT64_MAX) start[L.batch[m]] = step;
+             ++step;
+         },
+         [&](uint32_t k) { acc_at[k] = step; });
+    for (uint32_t k = 0; k < f.n_batches; ++k) {
+        uint32_t live = 1;
+        // per lane its batches start in order: count each lane's later batches begun before acc(k)
+        for (uint32_t l = 0; l < f.lanes; ++l) {
+            uint32_t j = k + 1 + (l + f.lanes - (k + 1) % f.lanes) % f.lanes;
+            for (; j < f.n_batches && start[j] < acc_at[k]; j += f.lanes) ++live;
+        }
+        f.ring = std::max(f.ring, live);
+    }
+    if ((uint64_t)f.ring * f.B > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "batch too large for the radiance ring (lower max_batch_items)");
+    if (f.cap > 0xFFFFFFFFull - 1024) throw Error(RS_E_INVALID, "path pool too large");
+    return f;
+}
+
 // One replica's share of a frame between enqueue and finish: multi-device renders enqueue every
 // replica before waiting for any, so the devices run concurrently.
 struct Pending {
     Replica* R = nullptr;
-    hipStream_t stream = nullptr;
+    Slot* L = nullptr;
+    hipStream_t stream = nullptr;   // the stream the frame ends on (the caller's, or the replica's own)
     bool empty = true;
-    bool wavefront = false, sorted = false, timed = false;
+    int kind = 0;                   // 0 megakernel, 1 bounce-synchronous wavefront, 2 streaming wavefront
+    bool timed = false;
     uint32_t n_pix = 0, N = 0, depth = 0, n_batches = 0, path_launches = 0;
     uint64_t n_chunks_total = 0;
+    std::vector<LaneSched> lanes;               // streaming: the lanes' schedules
+    std::vector<std::vector<uint32_t>> inj;     // streaming: camera samples injected per lane and iteration
     size_t ki = 0;
     std::vector<hipEvent_t> ev, kev;
     unsigned long long cnt[512];
@@ -1340,243 +1454,324 @@ void validate_render(const rs_scene* s, const rs_camera_desc* cam, const rs_rend
         throw Error(RS_E_INVALID, "frame too large");
 }
 
-// Enqueue the rows `rows` of the frame on replica R (its device must be current): batches of camera
-// samples -> wavefront or megakernel -> ordered accumulation -> into_color into d_out (W*H RGBA on
-// R's device). Nothing here waits for the device.
+hipStream_t lane_stream(Slot& L, uint32_t l) {
+    if (!L.lane[l]) HIP_OK(hipStreamCreateWithFlags(&L.lane[l], hipStreamNonBlocking));
+    if (!L.join_ev[l]) HIP_OK(hipEventCreateWithFlags(&L.join_ev[l], hipEventDisableTiming));
+    return L.lane[l];
+}
+
+// Enqueue the rows `rows` of the frame on replica R (its device must be current): camera samples ->
+// wavefront (streaming or bounce-synchronous) or megakernel -> ordered accumulation -> into_color into
+// d_out (W*H RGBA on R's device), the last step on `S`, the stream the frame ends on. The path work
+// runs on one of R's frame slots. Nothing here waits for the device.
 void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, const rs_render_settings* st,
-                    RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t stream, Pending& P, bool timed) {
+                    RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t S, Pending& P, bool timed) {
     P.R = &R;
-    P.stream = stream;
+    P.stream = S;
     P.timed = timed;
-    if (R.busy && R.busy_stream != stream) HIP_OK(hipStreamWaitEvent(stream, R.busy, 0));
-    const bool wavefront = st->mode != RS_MODE_MEGAKERNEL;
-    const uint32_t W = cam->width, H = cam->height;
     const uint32_t n_rows = rows.count();
     if (n_rows == 0) return;
     P.empty = false;
+    // one frame at a time for trees whose traversal stack spills to the replica's shared HBM overflow
+    const bool ext_spill = s->stack_need > kStackMax;
+    const uint32_t n_slots = ext_spill ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+    Slot& L = R.slots[R.next_slot % n_slots];
+    R.next_slot = (R.next_slot + 1) % n_slots;
+    P.L = &L;
+    const hipStream_t L0 = lane_stream(L, 0);
+    if (!L.free_ev) HIP_OK(hipEventCreateWithFlags(&L.free_ev, hipEventDisableTiming));
+    if (!L.entry_ev) HIP_OK(hipEventCreateWithFlags(&L.entry_ev, hipEventDisableTiming));
+    // the slot's previous frame must be done with its buffers; the caller's earlier work must be
+    // done when the kernels read the caller's memory (the mask); a timed frame runs alone
+    if (L.free_rec) HIP_OK(hipStreamWaitEvent(L0, L.free_ev, 0));
+    if (d_mask || timed) {
+        HIP_OK(hipEventRecord(L.entry_ev, S));
+        HIP_OK(hipStreamWaitEvent(L0, L.entry_ev, 0));
+    }
+    if (timed)
+        for (Slot& o : R.slots)
+            if (&o != &L && o.free_rec) HIP_OK(hipStreamWaitEvent(L0, o.free_ev, 0));
+
+    const bool wavefront = st->mode != RS_MODE_MEGAKERNEL;
+    const bool streaming = wavefront && streaming_mode(s->scene_mode);
+    const uint32_t W = cam->width, H = cam->height;
     const uint32_t n_pix = (uint32_t)((uint64_t)n_rows * W);
     const uint32_t sq = (uint32_t)std::floor(std::sqrt((double)st->samples));  // painter.rs:110-118
     const uint32_t N = sq * sq;
+    const uint32_t D = st->depth;
 
     DCamera dc = make_camera(*cam);
-    PathParams pp;
+    PathParams pp{};
     pp.n_pix_local = n_pix; pp.width = W; pp.height = H; pp.row_begin = rows.begin; pp.row_step = rows.step;
-    pp.sqrt_spp = sq; pp.depth = st->depth;
+    pp.sqrt_spp = sq; pp.depth = D;
     pp.key_base = splitmix64_h(splitmix64_h(st->seed) ^ (uint64_t)st->pass);
     pp.mask = d_mask;
-
-    uint32_t spb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(N, s->max_items_per_batch / n_pix));
-    if (N == 0) spb = 0;
-    ensure(R.d_acc, R.acc_cap, (size_t)3 * n_pix);
-    if (spb) ensure(R.d_rad, R.rad_cap, (size_t)3 * n_pix * spb);
-
-    const uint32_t n_batches = spb ? (N + spb - 1) / spb : 0;
-    // Wavefront lanes (RS_LANES, default 2): a batch's chunks go round-robin to lane streams and run
-    // concurrently, so one lane's launch tails and small late-bounce launches overlap the other's
-    // work (a strong-scaled share of a frame has many of those). Chunks are whole sample planes when
-    // the batch allows (camera-ray tile order, gen_perm). Scenes whose traversal stack spills to HBM
-    // keep one lane (the overflow array is shared by blockIdx).
-    const bool ext_spill = s->stack_need > kStackMax;
-    uint32_t lanes = (wavefront && N > 0 && !ext_spill) ? std::min<uint32_t>(kMaxLanes, s->wf_lanes) : 1u;
-    uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(s->wf_chunk, (uint64_t)n_pix * std::max(spb, 1u)));
-    if (lanes > 1) {
-        const uint64_t planes = (std::max(spb, 1u) + lanes - 1) / lanes;
-        const uint64_t split = std::max<uint64_t>(kBlock, spb >= lanes ? (uint64_t)n_pix * planes
-                                                                       : ((uint64_t)n_pix * spb + lanes - 1) / lanes);
-        chunk = std::min(chunk, split);
-    }
-    uint64_t n_chunks_total = 0;
-    for (uint32_t s0 = 0; s0 < N; s0 += spb) n_chunks_total += ((uint64_t)n_pix * std::min(spb, N - s0) + chunk - 1) / chunk;
-    if (n_chunks_total < lanes) lanes = std::max<uint32_t>(1, (uint32_t)n_chunks_total);
-    // material-sorted shading (k_wfs_*) for the spheres / nest-0 / nest-2 modes; flat scenes (meshes)
-    // are traversal-bound and run faster on the plain wavefront, whose extend kernel is lighter
-    // (mesh 480x270x16: 5.8 vs 7.2 ms; example.sdl 8.8 -> 7.6 ms, quadric.sdl 9.9 -> 8.9 ms sorted)
-    const bool sorted = wavefront && (s->scene_mode == kSmSpheres || s->scene_mode == kSmNest0 ||
-                                      s->scene_mode == kSmNest2 || (RS_SORTED_FLAT && s->scene_mode == kSmFlat));
-    const uint32_t cstride = sorted ? kWfsStride : 1;
-    // phased extend (flat scenes with a 4-wide tree whose stack fits LDS): one continuation counter
-    // per (chunk, bounce, bounded phase), each on its own 128-byte line, after the queue counters
-    const bool phased = wavefront && !sorted && s->scene_mode == kSmFlat && s->ph_n > 0 && s->tree_arity == 4 &&
-                        s->stack_need + 3 <= kStackMax;
-    const size_t cc_base = (size_t)n_chunks_total * (st->depth + 1) * cstride;
-    const size_t n_cc = phased ? (size_t)n_chunks_total * st->depth * s->ph_n * 32 : 0;
-    hipStream_t ls[kMaxLanes] = {stream};
-    if (wavefront && N > 0) {
-        carve_wf(R, chunk, lanes);
-        const size_t nc = (size_t)n_chunks_total * (st->depth + 1) * cstride + n_cc;
-        uint32_t* const prev_counts = R.d_counts;
-        ensure(R.d_counts, R.counts_cap, nc);
-        if (R.d_counts != prev_counts) R.counts_clean = 0;
-        if (phased) carve_cont(R, R.wf_cap, lanes, s->stack_need);
-        for (uint32_t l = 1; l < lanes; ++l) {
-            if (!R.lane_stream[l]) HIP_OK(hipStreamCreateWithFlags(&R.lane_stream[l], hipStreamNonBlocking));
-            if (!R.join_ev[l]) HIP_OK(hipEventCreateWithFlags(&R.join_ev[l], hipEventDisableTiming));
-            ls[l] = R.lane_stream[l];
-        }
-        if (lanes > 1 && !R.fork_ev) HIP_OK(hipEventCreateWithFlags(&R.fork_ev, hipEventDisableTiming));
-    }
-    // launch grids: grid-stride kernels over at most these many blocks
-    const uint32_t ext_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.ext_bpc));
-    const uint32_t shade_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.shade_bpc));
-#ifndef RS_WIDE_BPC
-#define RS_WIDE_BPC 64  // shading grids (their queue lengths live on the device): 8 -> 64 per CU, 9.22 -> 9.12 ms
-#endif
-    const uint32_t wide = (uint32_t)std::max(1, R.n_cu * RS_WIDE_BPC);
-    // sorted-path extend grids: one block per 256 paths, so no block loops over batches and the hardware
-    // dispatcher refills a CU as soon as one of its blocks ends (bench frame 9.58 -> 9.22 ms against a
-    // grid-stride loop over 8 blocks per CU). A tree deeper than the LDS stack part spills to an HBM
-    // array strided by the grid's threads: such scenes keep a bounded grid-stride grid.
-#ifndef RS_WF_FULL
-#define RS_WF_FULL 1  // meshes: lock-step extend one block per 256 paths, shading 64 blocks/CU (C5 49.6 -> 48.1 ms)
-#endif
-    const bool wf_full = RS_WF_FULL && s->scene_mode == kSmFlat;  // lock-step unsorted grids (meshes only)
-    auto ext_grid = [&](uint32_t n) {
-        const uint32_t b = (n + kBlock - 1) / kBlock;
-        return ext_spill ? std::min(wide, b) : b;
-    };
-    const uint32_t mega_blocks = wide;
-    ensure_stack_overflow(s, R, (uint64_t)std::max(std::max(ext_blocks, shade_blocks), wide) * kBlock);
-    const size_t n_kernel_ev = wavefront ? (size_t)n_chunks_total * st->depth : n_batches;
-    // timing events only when the caller asks for stats (they cost a gap of ~6 us per event packet;
-    // the extend launches carry theirs in the dispatch itself, hipExtLaunchKernel)
-    P.ev.assign(timed ? 2 * (size_t)n_batches : 0, nullptr);
-    P.kev.assign(timed ? 2 * n_kernel_ev : 0, nullptr);
-    for (auto& e : P.ev) HIP_OK(hipEventCreate(&e));
-    for (auto& e : P.kev) HIP_OK(hipEventCreate(&e));
-    auto kev = [&](size_t i) -> hipEvent_t { return timed ? P.kev[i] : nullptr; };
-    auto record = [&](size_t i) { if (timed) HIP_OK(hipEventRecord(P.ev[i], stream)); };
-    const SceneRef ds = R.ref();
-    // the megakernel's segment counters; the wavefront's queue counters start zeroed -- either the
-    // previous frame's last accumulate reset them (counts_clean) or a memset does it here
-    if (!wavefront || timed) HIP_OK(hipMemsetAsync(R.d_cnt, 0, 512 * sizeof(unsigned long long), stream));
-    const size_t n_counts = wavefront && N > 0 ? cc_base + n_cc : 0;
-    if (n_counts > R.counts_clean) HIP_OK(hipMemsetAsync(R.d_counts, 0, n_counts * sizeof(uint32_t), stream));
-    R.counts_clean = 0;
-    if (N == 0) HIP_OK(hipMemsetAsync(R.d_acc, 0, (size_t)3 * n_pix * sizeof(double), stream));
     FinalParams fp;
     fp.n_pix_local = n_pix; fp.width = W; fp.row_begin = rows.begin; fp.row_step = rows.step; fp.n_samples = N;
     fp.gamma = st->gamma; fp.mask = d_mask;
-    uint32_t bi = 0;
+
+    const uint32_t spb = N ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(N, s->max_items_per_batch / n_pix)) : 0;
+    const uint32_t n_batches = spb ? (N + spb - 1) / spb : 0;
+    ensure(L, L.d_acc, L.acc_cap, (size_t)3 * n_pix);
+    if (!L.d_cnt) HIP_OK(hipMalloc((void**)&L.d_cnt, 512 * sizeof(unsigned long long)));
+    // launch grids: grid-stride kernels over at most these many blocks (shading grids and the
+    // streaming extend: 64 per CU; 8 -> 64 measured 9.22 -> 9.12 ms on the bench frame in round 2)
+    const uint32_t wide = (uint32_t)std::max(1, R.n_cu * 64);
+    // the streaming extend: one block per 256 paths (a grid-stride loop over fewer blocks waits at the
+    // queue barriers for its slowest wave, batch after batch); a bounded grid where the traversal stack
+    // spills to the HBM overflow array, which is sized by grid threads
+    const uint32_t ext_cap = ext_spill ? wide : 0xFFFFFFFFu;
+    const uint32_t ext_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.ext_bpc));
+    const uint32_t shade_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.shade_bpc));
+    ensure_stack_overflow(s, R, (uint64_t)std::max(std::max(ext_blocks, shade_blocks), wide) * kBlock);
+    const SceneRef ds = R.ref();
+    const int sm = s->scene_mode;
+
+    auto new_ev = [&]() { hipEvent_t e; HIP_OK(hipEventCreate(&e)); return e; };
+    // the frame's end on S: join L0 into S, then the last accumulate there (it writes the caller's frame)
+    auto join_to_S = [&]() {
+        if (S == L0) return;
+        HIP_OK(hipEventRecord(L.join_ev[0], L0));
+        HIP_OK(hipStreamWaitEvent(S, L.join_ev[0], 0));
+    };
     size_t ki = 0;
-    uint64_t chunk_i = 0;
     uint32_t path_launches = 0;
-    for (uint32_t s0 = 0; s0 < N; s0 += spb, ++bi) {
-        const uint32_t nb = std::min(spb, N - s0);
-        pp.s0 = s0;
-        pp.n_items = (uint64_t)n_pix * nb;
-        record(2 * bi);
-        if (!wavefront) {
-            if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], stream));
-            HIP_OK(launch_path_mega(ds, dc, pp, s->scene_mode, R.d_rad, R.d_cnt, mega_blocks, stream));
-            if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], stream));
-            ++ki;
-            ++path_launches;
-        } else {
-            if (lanes > 1) {  // fork: the lane streams start after what `stream` holds
-                HIP_OK(hipEventRecord(R.fork_ev, stream));
-                for (uint32_t l = 1; l < lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], R.fork_ev, 0));
-            }
-            uint32_t lane = 0;
-            for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i, lane = (lane + 1) % lanes) {
-                const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, pp.n_items - c0);
-                WfState WS = R.lane_ws[lane];
-                WS.counts = R.d_counts + chunk_i * (st->depth + 1) * cstride;
-                hipStream_t cs = ls[lane];
-                uint32_t** qd = R.d_qptrs[lane];
-                if (!sorted) {  // the sorted path generates camera rays inside its bounce-0 extend
-                    HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, R.d_rad, cs));
-                    ++path_launches;
+    size_t n_counts = 0;
+
+    if (N == 0) {  // no samples: into_color of 0 / 0 (NaN, or 0 with the mask) for every lattice pixel
+        HIP_OK(hipMemsetAsync(L.d_acc, 0, (size_t)3 * n_pix * sizeof(double), L0));
+        join_to_S();
+        HIP_OK(launch_finalize(L.d_acc, d_out, fp, S));
+    } else if (streaming) {
+        const FrameSched f = make_sched(s, n_pix, N, D, ext_spill ? 1u : std::min<uint32_t>(kMaxLanes, s->stream_lanes));
+        ensure(L, L.d_rad, L.rad_cap, (size_t)3 * f.ring * f.B);
+        carve_wf(L, f.cap, f.lanes);
+        n_counts = f.n_counts;
+        uint32_t* const prev_counts = L.d_counts;
+        ensure(L, L.d_counts, L.counts_cap, n_counts);
+        if (L.d_counts != prev_counts) L.counts_clean = 0;
+        if (n_counts > L.counts_clean) HIP_OK(hipMemsetAsync(L.d_counts, 0, n_counts * sizeof(uint32_t), L0));
+        L.counts_clean = 0;
+        // every lane and the accumulate stream start after L0's dependencies and the counter reset
+        hipStream_t ls[kMaxLanes] = {L0};
+        for (uint32_t l = 1; l < f.lanes; ++l) ls[l] = lane_stream(L, l);
+        if (!L.acc_stream) HIP_OK(hipStreamCreateWithFlags(&L.acc_stream, hipStreamNonBlocking));
+        if (!L.fork_ev) HIP_OK(hipEventCreateWithFlags(&L.fork_ev, hipEventDisableTiming));
+        HIP_OK(hipEventRecord(L.fork_ev, L0));
+        for (uint32_t l = 1; l < f.lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], L.fork_ev, 0));
+        HIP_OK(hipStreamWaitEvent(L.acc_stream, L.fork_ev, 0));
+        // per batch: its paths are done (recorded on its lane) / it has been accumulated (acc stream)
+        while (L.bev.size() < 2 * (size_t)f.n_batches) {
+            hipEvent_t e;
+            HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            L.bev.push_back(e);
+        }
+        auto done_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k]; };
+        auto acc_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k + 1]; };
+        const bool split = ext_split(sm) || s->ext_split;
+        size_t n_ext = 0;
+        for (const LaneSched& ln : f.lane) n_ext += ln.T * (split ? 2 : 1);
+        P.kev.assign(timed ? 2 * n_ext : 0, nullptr);
+        for (auto& e : P.kev) e = new_ev();
+        P.ev.assign(timed ? 2 : 0, nullptr);  // path_ms: the frame's iterations
+        for (auto& e : P.ev) e = new_ev();
+        if (timed) HIP_OK(hipEventRecord(P.ev[0], L0));
+        P.lanes.assign(f.lane.begin(), f.lane.end());
+        // per lane: the samples injected by its last depth - 1 iterations (a bound on the paths it
+        // carries into the next one), its next batch to be done, and the injections per iteration
+        std::vector<uint64_t> window(f.lanes, 0), m_done(f.lanes, 0);
+        std::vector<std::vector<uint32_t>> inj(f.lanes);
+        for (uint32_t l = 0; l < f.lanes; ++l) inj[l].assign(f.lane[l].T, 0u);
+        const uint64_t ring_items = (uint64_t)f.ring * f.B;
+        walk(f,
+             [&](uint32_t l, uint64_t t) {
+                 const LaneSched& ln = f.lane[l];
+                 const hipStream_t cs = ls[l];
+                 WfState WS = L.lane_ws[l];
+                 WS.counts = L.d_counts + ln.cnt_off;
+                 uint32_t** qd = L.d_qptrs[l];
+                 const uint32_t n_new = ln.n_new(t);
+                 inj[l][t] = n_new;
+                 InjParams I{};
+                 I.n_new = n_new;
+                 I.ring = ring_items;
+                 if (n_new) {
+                     const uint64_t j0 = t * ln.Q, m = j0 / f.B;
+                     const uint32_t k = ln.batch[m];
+                     I.jb0 = (uint32_t)(j0 - m * f.B);
+                     I.nb0 = (uint32_t)ln.nb(m);
+                     I.nb1 = m + 1 < ln.batch.size() ? (uint32_t)ln.nb(m + 1) : 0u;
+                     I.g0 = (uint64_t)k * f.B;
+                     I.g1 = m + 1 < ln.batch.size() ? (uint64_t)ln.batch[m + 1] * f.B : 0u;
+                     I.rad0 = (uint32_t)((k % f.ring) * f.B);
+                     I.rad1 = m + 1 < ln.batch.size() ? (uint32_t)((ln.batch[m + 1] % f.ring) * f.B) : 0u;
+                     // a batch taking over a ring buffer: after the batch `ring` earlier was accumulated
+                     for (uint64_t mm = m; mm <= m + 1 && mm < ln.batch.size(); ++mm) {
+                         const uint32_t kk = ln.batch[mm];
+                         if (ln.first_it(mm) == t && kk >= f.ring) HIP_OK(hipStreamWaitEvent(cs, acc_ev(kk - f.ring), 0));
+                     }
+                 }
+                 auto extend = [&](int part, uint64_t n_max) {
+                     const uint32_t b = (uint32_t)std::min<uint64_t>(ext_cap, (n_max + kBlock - 1) / kBlock);
+                     if (!b) return;
+                     HIP_OK(launch_wfs_extend(ds, dc, pp, WS, qd, (uint32_t)t, I, L.d_rad, b, part, sm, cs,
+                                              timed ? P.kev[2 * ki] : nullptr, timed ? P.kev[2 * ki + 1] : nullptr));
+                     ++ki;
+                     ++path_launches;
+                 };
+                 if (split) {
+                     extend(kExtCarried, window[l]);
+                     extend(kExtCamera, n_new);
+                 } else {
+                     extend(kExtAll, window[l] + n_new);
+                 }
+                 if (D > 0) {
+                     const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + n_new + kBlock - 1) / kBlock);
+                     HIP_OK(launch_wfs_shade_all(ds, WS, qd, s->class_mask, (uint32_t)t, D, ring_items, L.d_rad, b, sm, cs));
+                     ++path_launches;
+                 }
+                 // carried into t + 1: the samples injected by iterations t - depth + 2 .. t
+                 window[l] += n_new;
+                 if (D == 0) window[l] = 0;
+                 else if (t + 1 >= D) window[l] -= inj[l][t + 1 - D];
+                 while (m_done[l] < ln.batch.size() && ln.done_it(m_done[l]) == t)
+                     HIP_OK(hipEventRecord(done_ev(ln.batch[m_done[l]++]), cs));
+             },
+             [&](uint32_t k) {
+                 // batch k's samples have all finished: accumulate in sample order (the last batch on S,
+                 // writing the frame and zeroing the counters for the next frame unless statistics read them)
+                 const uint32_t planes = (uint32_t)(std::min<uint64_t>(f.B, (uint64_t)n_pix * N - (uint64_t)k * f.B) / n_pix);
+                 const double* rk = L.d_rad + (size_t)(k % f.ring) * f.B;
+                 if (k + 1 < f.n_batches) {
+                     HIP_OK(hipStreamWaitEvent(L.acc_stream, done_ev(k), 0));
+                     HIP_OK(launch_accumulate(rk, ring_items, L.d_acc, n_pix, planes, k == 0, 0, fp, d_out, nullptr, 0,
+                                              L.acc_stream));
+                     HIP_OK(hipEventRecord(acc_ev(k), L.acc_stream));
+                 } else {
+                     HIP_OK(hipEventRecord(L.join_ev[0], L.acc_stream));
+                     HIP_OK(hipStreamWaitEvent(S, L.join_ev[0], 0));
+                     HIP_OK(hipStreamWaitEvent(S, done_ev(k), 0));
+                     for (uint32_t l = 1; l < f.lanes; ++l) {  // (every lane's last iteration, for the counters)
+                         HIP_OK(hipEventRecord(L.join_ev[l], ls[l]));
+                         HIP_OK(hipStreamWaitEvent(S, L.join_ev[l], 0));
+                     }
+                     HIP_OK(hipEventRecord(L.fork_ev, L0));
+                     HIP_OK(hipStreamWaitEvent(S, L.fork_ev, 0));
+                     const size_t nz = timed ? 0 : n_counts;
+                     HIP_OK(launch_accumulate(rk, ring_items, L.d_acc, n_pix, planes, k == 0, 1, fp, d_out, L.d_counts,
+                                              (uint32_t)nz, S));
+                     L.counts_clean = nz;
+                 }
+             });
+        P.inj = std::move(inj);
+        if (timed) HIP_OK(hipEventRecord(P.ev[1], S));
+    } else {
+        // bounce-synchronous wavefront (flat / rich scenes) or megakernel: per batch of spb sample planes
+        ensure(L, L.d_rad, L.rad_cap, (size_t)3 * n_pix * spb);
+        // Wavefront lanes (rs_scene_set_lanes, default 2): a batch's chunks go round-robin to lane streams
+        // and run concurrently, so one lane's launch tails and small late-bounce launches overlap the
+        // other's work. Chunks are whole sample planes when the batch allows (camera-ray tile order,
+        // gen_perm). Scenes whose traversal stack spills to HBM keep one lane (the overflow array is
+        // shared by blockIdx).
+        uint32_t lanes = (wavefront && !ext_spill) ? std::min<uint32_t>(kMaxLanes, s->wf_lanes) : 1u;
+        uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(s->pool_paths, (uint64_t)n_pix * spb));
+        if (lanes > 1) {
+            const uint64_t planes = (spb + lanes - 1) / lanes;
+            const uint64_t split = std::max<uint64_t>(kBlock, spb >= lanes ? (uint64_t)n_pix * planes
+                                                                           : ((uint64_t)n_pix * spb + lanes - 1) / lanes);
+            chunk = std::min(chunk, split);
+        }
+        uint64_t n_chunks_total = 0;
+        for (uint32_t s0 = 0; s0 < N; s0 += spb) n_chunks_total += ((uint64_t)n_pix * std::min(spb, N - s0) + chunk - 1) / chunk;
+        if (n_chunks_total < lanes) lanes = std::max<uint32_t>(1, (uint32_t)n_chunks_total);
+        hipStream_t ls[kMaxLanes] = {L0};
+        if (wavefront) {
+            carve_wf(L, chunk, lanes);
+            n_counts = (size_t)n_chunks_total * (D + 1);
+            uint32_t* const prev_counts = L.d_counts;
+            ensure(L, L.d_counts, L.counts_cap, n_counts);
+            if (L.d_counts != prev_counts) L.counts_clean = 0;
+            for (uint32_t l = 1; l < lanes; ++l) ls[l] = lane_stream(L, l);
+            if (lanes > 1 && !L.fork_ev) HIP_OK(hipEventCreateWithFlags(&L.fork_ev, hipEventDisableTiming));
+        }
+        P.ev.assign(timed ? 2 * (size_t)n_batches : 0, nullptr);
+        for (auto& e : P.ev) e = new_ev();
+        P.kev.assign(timed ? 2 * (wavefront ? (size_t)n_chunks_total * D : n_batches) : 0, nullptr);
+        for (auto& e : P.kev) e = new_ev();
+        if (!wavefront || timed) HIP_OK(hipMemsetAsync(L.d_cnt, 0, 512 * sizeof(unsigned long long), L0));
+        if (n_counts > L.counts_clean) HIP_OK(hipMemsetAsync(L.d_counts, 0, n_counts * sizeof(uint32_t), L0));
+        L.counts_clean = 0;
+        uint32_t bi = 0;
+        uint64_t chunk_i = 0;
+        for (uint32_t s0 = 0; s0 < N; s0 += spb, ++bi) {
+            const uint32_t nb = std::min(spb, N - s0);
+            pp.s0 = s0;
+            pp.n_items = (uint64_t)n_pix * nb;
+            if (timed) HIP_OK(hipEventRecord(P.ev[2 * bi], L0));
+            if (!wavefront) {
+                if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], L0));
+                HIP_OK(launch_path_mega(ds, dc, pp, sm, L.d_rad, L.d_cnt, wide, L0));
+                if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], L0));
+                ++ki;
+                ++path_launches;
+            } else {
+                if (lanes > 1) {  // fork: the lane streams start after what L0 holds
+                    HIP_OK(hipEventRecord(L.fork_ev, L0));
+                    for (uint32_t l = 1; l < lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], L.fork_ev, 0));
                 }
-                for (uint32_t b = 0; sorted && b < st->depth; ++b) {
-                    if (b == 0)
-                        HIP_OK(launch_wfs_gen_extend(ds, dc, pp, WS, qd, cstride, c0, n, R.d_rad,
-                                                     ext_grid(n), s->scene_mode, cs, kev(2 * ki), kev(2 * ki + 1)));
-                    else
-                        HIP_OK(launch_wfs_extend(ds, WS, qd, b, cstride, pp.n_items, R.d_rad,
-                                                 ext_grid(n), s->scene_mode, cs, kev(2 * ki),
-                                                 kev(2 * ki + 1)));
-                    ++ki;
+                uint32_t lane = 0;
+                for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i, lane = (lane + 1) % lanes) {
+                    const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, pp.n_items - c0);
+                    WfState WS = L.lane_ws[lane];
+                    WS.counts = L.d_counts + chunk_i * (D + 1);
+                    const hipStream_t cs = ls[lane];
+                    HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, L.d_rad, cs));
                     ++path_launches;
-                    // (the classes' shading kernels on side streams, concurrently after the extend,
-                    // measured slower: bench frame 10.24 -> 10.32 ms)
-                    const uint32_t shade_grid = std::min(wide, (n + kBlock - 1) / kBlock);
-                    if (RS_SHADE_MERGED) {
-                        // classes kShadeAllFirst .. 3 in one launch; the others (Lambertian in mode 2,
-                        // the generic class 4) in their own
-                        const uint32_t merged = s->class_mask & (0xFu & ~((1u << kShadeAllFirst) - 1u));
-                        for (int k = 0; k < kWfsClasses; ++k) {
-                            if (!(s->class_mask & (1u << k)) || (merged & (1u << k))) continue;
-                            HIP_OK(launch_wfs_shade(ds, WS, R.qptr[lane][k], k, b, cstride, st->depth, pp.n_items, R.d_rad,
-                                                    shade_grid, s->scene_mode, cs));
-                            ++path_launches;
-                        }
-                        if (merged) {
-                            HIP_OK(launch_wfs_shade_all(ds, WS, qd, merged, b, cstride, st->depth, pp.n_items,
-                                                        R.d_rad, shade_grid, s->scene_mode, cs));
-                            ++path_launches;
-                        }
-                    } else {
-                        for (int k = 0; k < kWfsClasses; ++k) {
-                            if (!(s->class_mask & (1u << k))) continue;  // no prim of this class: empty queue
-                            HIP_OK(launch_wfs_shade(ds, WS, R.qptr[lane][k], k, b, cstride, st->depth, pp.n_items, R.d_rad,
-                                                    shade_grid, s->scene_mode, cs));
-                            ++path_launches;
-                        }
-                    }
-                }
-                for (uint32_t b = 0; !sorted && b < st->depth; ++b) {
-                    if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
-                    if (phased) {
-                        // phase 0 over the bounce's paths, phases 1.. over the previous phase's
-                        // suspended traversals (ping-pong sets), the last one to the end
-                        uint32_t* cc = R.d_counts + cc_base + ((chunk_i * st->depth + b) * s->ph_n) * 32;
-                        const uint32_t g = ext_grid(n);
-                        for (int p = 0; p <= s->ph_n; ++p) {
-                            const bool last = p == s->ph_n;
-                            HIP_OK(launch_wf_extend_ph(ds, WS, b, R.cont[lane][(p + 1) & 1], p ? cc + (p - 1) * 32 : nullptr,
-                                                       R.cont[lane][p & 1], last ? nullptr : cc + p * 32,
-                                                       last ? -1 : s->ph_budget[p], g, cs));
-                            ++path_launches;
-                        }
-                        --path_launches;
-                    } else {
+                    for (uint32_t b = 0; b < D; ++b) {
+                        if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
+                        // meshes: one block per 256 paths (C5 49.6 -> 48.1 ms); the rich mode a bounded grid
                         HIP_OK(launch_wf_extend(ds, WS, b,
-                                                wf_full ? ext_grid(n) : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
-                                                s->scene_mode, cs));
+                                                sm == kSmFlat && !ext_spill ? (n + kBlock - 1) / kBlock
+                                                                            : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
+                                                sm, cs));
+                        if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
+                        ++ki;
+                        HIP_OK(launch_wf_shade(ds, WS, b, D, pp.n_items, L.d_rad,
+                                               std::min(sm == kSmFlat ? wide : shade_blocks, (n + kBlock - 1) / kBlock),
+                                               sm, cs));
+                        path_launches += 2;
                     }
-                    if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
-                    ++ki;
-                    HIP_OK(launch_wf_shade(ds, WS, b, st->depth, pp.n_items, R.d_rad,
-                                           std::min(wf_full ? wide : shade_blocks, (n + kBlock - 1) / kBlock), s->scene_mode, cs));
-                    path_launches += 2;
+                }
+                if (lanes > 1) {  // join: L0 continues after every lane's chunks
+                    for (uint32_t l = 1; l < lanes; ++l) {
+                        HIP_OK(hipEventRecord(L.join_ev[l], ls[l]));
+                        HIP_OK(hipStreamWaitEvent(L0, L.join_ev[l], 0));
+                    }
                 }
             }
-            if (lanes > 1) {  // join: `stream` continues after every lane's chunks
-                for (uint32_t l = 1; l < lanes; ++l) {
-                    HIP_OK(hipEventRecord(R.join_ev[l], ls[l]));
-                    HIP_OK(hipStreamWaitEvent(stream, R.join_ev[l], 0));
-                }
+            if (timed) HIP_OK(hipEventRecord(P.ev[2 * bi + 1], L0));
+            const bool last = s0 + spb >= N;
+            if (!last) {
+                HIP_OK(launch_accumulate(L.d_rad, pp.n_items, L.d_acc, n_pix, nb, s0 == 0, 0, fp, d_out, nullptr, 0, L0));
+            } else {
+                // the last batch's accumulate finishes the frame (into_color) and, when no statistics
+                // read the queue counters afterwards, zeroes them for the next frame (no memset launch)
+                join_to_S();
+                const size_t nz = (wavefront && !timed) ? n_counts : 0;
+                HIP_OK(launch_accumulate(L.d_rad, pp.n_items, L.d_acc, n_pix, nb, s0 == 0, 1, fp, d_out, L.d_counts,
+                                         (uint32_t)nz, S));
+                L.counts_clean = nz;
             }
         }
-        record(2 * bi + 1);
-        // the last batch's accumulate finishes the frame (into_color) and, when no statistics read
-        // the queue counters afterwards, zeroes them for the next frame (no memset launch there)
-        const bool last = s0 + spb >= N;
-        const size_t nz = (last && !timed) ? n_counts : 0;
-        HIP_OK(launch_accumulate(R.d_rad, R.d_acc, n_pix, nb, s0 == 0, last, fp, d_out, R.d_counts, (uint32_t)nz, stream));
-        if (last) R.counts_clean = nz;
+        P.n_chunks_total = n_chunks_total;
     }
-    if (N == 0) HIP_OK(launch_finalize(R.d_acc, d_out, fp, stream));
-    if (!R.busy) HIP_OK(hipEventCreateWithFlags(&R.busy, hipEventDisableTiming));
-    HIP_OK(hipEventRecord(R.busy, stream));
-    R.busy_stream = stream;
-    P.wavefront = wavefront;
-    P.sorted = sorted;
+    HIP_OK(hipEventRecord(L.free_ev, S));
+    L.free_rec = true;
+    P.kind = !wavefront ? 0 : streaming ? 2 : 1;
     P.n_pix = n_pix;
     P.N = N;
-    P.depth = st->depth;
+    P.depth = D;
     P.n_batches = n_batches;
-    P.n_chunks_total = n_chunks_total;
     P.ki = ki;
     P.path_launches = path_launches;
 }
@@ -1585,18 +1780,19 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
 void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
     if (P.empty) return;
     if (!P.timed || !stats) { HIP_OK(hipStreamSynchronize(P.stream)); return; }
-    Replica& R = *P.R;
-    HIP_OK(hipMemcpyAsync(P.cnt, R.d_cnt, sizeof(P.cnt), hipMemcpyDeviceToHost, P.stream));
-    const uint32_t cstride_f = P.sorted ? kWfsStride : 1;
-    P.qc.assign(P.wavefront && P.N > 0 ? (size_t)P.n_chunks_total * (P.depth + 1) * cstride_f : 0, 0u);
-    if (!P.qc.empty())
-        HIP_OK(hipMemcpyAsync(P.qc.data(), R.d_counts, P.qc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, P.stream));
+    Slot& L = *P.L;
+    HIP_OK(hipMemcpyAsync(P.cnt, L.d_cnt, sizeof(P.cnt), hipMemcpyDeviceToHost, P.stream));
+    size_t words = 0;
+    if (P.N > 0 && P.kind == 2)
+        for (const LaneSched& ln : P.lanes) words = std::max<size_t>(words, ln.cnt_off + (ln.T + 1) * kWfsStride);
+    if (P.N > 0 && P.kind == 1) words = (size_t)P.n_chunks_total * (P.depth + 1);
+    P.qc.assign(words, 0u);
+    if (words) HIP_OK(hipMemcpyAsync(P.qc.data(), L.d_counts, words * sizeof(uint32_t), hipMemcpyDeviceToHost, P.stream));
     HIP_OK(hipStreamSynchronize(P.stream));
-    if (!stats) return;
     double path_ms = 0.0;
-    for (uint32_t b = 0; b < P.n_batches; ++b) {
+    for (size_t b = 0; b + 1 < P.ev.size(); b += 2) {
         float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, P.ev[2 * b], P.ev[2 * b + 1]));
+        HIP_OK(hipEventElapsedTime(&ms, P.ev[b], P.ev[b + 1]));
         path_ms += ms;
     }
     double kernel_ms = 0.0;
@@ -1605,47 +1801,37 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         HIP_OK(hipEventElapsedTime(&ms, P.kev[2 * k], P.kev[2 * k + 1]));
         kernel_ms += ms;
     }
-    uint64_t seg = 0;
-    for (int i = 0; i < 256; ++i) seg += P.cnt[i];
-    uint64_t cont = 0, seg0 = 0, cont0 = 0;
-    if (!P.qc.empty()) {  // segments = sum over bounces of the extend queue lengths
-        seg = 0;
-        for (uint64_t c = 0; c < P.n_chunks_total; ++c)
-            for (uint32_t b = 0; b < P.depth; ++b) {
-                const uint32_t* q = &P.qc[(c * (P.depth + 1) + b) * cstride_f];
-                uint64_t cb = 0;
-                if (cstride_f > 1)
-                    for (int k = 0; k < kWfsClasses; ++k)
-                        for (uint32_t g = 0; g < kQSub; ++g) cb += q[cix(1 + k, g)];
-                uint64_t live = q[0];  // bounces >= 1; bounce 0 counts on kStatLines lines
-                if (cstride_f > 1)
-                    for (uint32_t k = 0; k < kStatLines; ++k) live += q[cix(kCntStat0 + (int)k)];
-                if (b == 0) { seg0 += live; cont0 += cb; }
-                seg += live;
-                cont += cb;
-            }
-    }
-    // algorithmic bytes of the dominant kernel (DESIGN.md Roofline):
-    //  megakernel   : radiance out, 3 x f64 per sample
-    //  wf extend    : ray in (2 x 32 B records) + hit out (16 B) per segment
-    //  wfs extend   : bounces >= 1: ray in (64 B) per segment; + hit (16 B) + queue slot (4 B)
-    //                 per shaded segment; + throughput record in (32 B), item (4 B) and
-    //                 radiance out (24 B) per path ending in extend (sky miss / light hit).
-    //                 bounce 0 (fused with ray generation): radiance out (24 B) per sample that
-    //                 ends there (incl. masked); hit + queue slot + ray records (64 B, rng
-    //                 inside) + throughput record (32 B) + item (4 B) per shaded one
     const uint64_t items = (uint64_t)P.n_pix * P.N;
-    uint64_t kbytes;
-    if (!P.wavefront) {
+    uint64_t seg = 0, kbytes = 0;
+    if (P.kind == 0) {
+        for (int i = 0; i < 256; ++i) seg += P.cnt[i];
         stats->kernel_id = RS_KERNEL_PATH_MEGA;
-        kbytes = 24ull * items;
-    } else if (cstride_f > 1) {
-        stats->kernel_id = RS_KERNEL_WFS_EXTEND;
-        const uint64_t segr = seg - seg0, contr = cont - cont0;
-        kbytes = 24ull * (items - cont0) + 120ull * cont0 + 64ull * segr + 20ull * contr + 60ull * (segr - contr);
-    } else {
+        kbytes = 24ull * items;  // radiance out, 3 x f64 per sample
+    } else if (P.kind == 1) {
+        // segments = sum over chunks and bounces of the extend queue lengths; the extend reads a ray
+        // (2 x 32 B records) and writes a hit (16 B) per segment
+        for (uint64_t c = 0; c < P.n_chunks_total; ++c)
+            for (uint32_t b = 0; b < P.depth; ++b) seg += P.qc[c * (P.depth + 1) + b];
         stats->kernel_id = RS_KERNEL_WF_EXTEND;
         kbytes = 80ull * seg;
+    } else {
+        // the streaming extend's library byte model, per iteration: ray records in (64 B)
+        // per carried path; hit (16 B) + queue slot (4 B) per shaded segment; the record out (96 B + item
+        // + level) per live camera sample (written before its traversal); radiance out (24 B) per path
+        // ending in extend, + its throughput record and item in (36 B); radiance out for masked samples
+        for (size_t l = 0; l < P.lanes.size(); ++l)
+            for (uint64_t t = 0; t < P.lanes[l].T; ++t) {
+                const uint32_t* q = &P.qc[P.lanes[l].cnt_off + t * kWfsStride];
+                uint64_t live = 0, shaded = 0;
+                for (uint32_t k = 0; k < kStatLines; ++k) live += q[cix(kCntStat0 + (int)k)];
+                for (int k = 0; k < kWfsClasses; ++k) shaded += q[cix(1 + k)];
+                const uint64_t old = q[cix(0)];
+                const uint64_t live_new = live - old, dead_new = P.inj[l][t] - live_new;
+                const uint64_t ended = live - shaded;
+                seg += live;
+                kbytes += 64ull * old + 20ull * shaded + 104ull * live_new + 60ull * ended + 24ull * dead_new;
+            }
+        stats->kernel_id = RS_KERNEL_WFS_EXTEND;
     }
     stats->path_ms += path_ms;
     stats->launches += P.path_launches;
@@ -1666,8 +1852,9 @@ hipError_t copy_rows(float* dst, const float* src, uint32_t W, RowSet rows, hipM
     return hipMemcpy2DAsync(dst + off, row_bytes * rows.step, src + off, row_bytes * rows.step, row_bytes, n, kind, st);
 }
 
-// rs_render_device: replica 0 renders its rows straight into d_out on the caller's stream; every
-// other replica renders into its own frame on its own stream and copies its rows into d_out.
+// rs_render_device: replica 0 renders its rows straight into d_out, its frame ending on the caller's
+// stream; every other replica renders into a frame of its own device (its slot's) ending on its own
+// stream and copies its rows into d_out.
 void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* d_mask,
                          float* d_out, hipStream_t stream, rs_render_stats* stats) {
     if (!d_out) throw Error(RS_E_INVALID, "null argument");
@@ -1695,17 +1882,23 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
                 continue;
             }
             if (rows.count() == 0) continue;
-            // the side streams read d_mask and write d_out: order them after the caller's work
+            // the replica's stream reads d_mask and writes d_out: order it after the caller's work
             HIP_OK(hipStreamWaitEvent(R.stream, entry, 0));
-            ensure(R.d_out, R.out_cap, npx * 4);
+            // this frame's copies of the mask and the frame live in R's next slot (the slot render_enqueue
+            // picks): its previous frame must be done with them
+            const uint32_t n_slots = s->stack_need > kStackMax ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            Slot& L = R.slots[R.next_slot % n_slots];
+            if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
+            ensure(L, L.d_out, L.out_cap, npx * 4);
             const uint8_t* m = nullptr;
             if (d_mask) {
-                ensure(R.d_mask, R.mask_cap, npx);
-                HIP_OK(hipMemcpyAsync(R.d_mask, d_mask, npx, hipMemcpyDefault, R.stream));
-                m = R.d_mask;
+                ensure(L, L.d_mask, L.mask_cap, npx);
+                HIP_OK(hipMemcpyAsync(L.d_mask, d_mask, npx, hipMemcpyDefault, R.stream));
+                m = L.d_mask;
             }
-            render_enqueue(s, R, cam, st, rows, m, R.d_out, R.stream, *P[k], stats != nullptr);
-            HIP_OK(copy_rows(d_out, R.d_out, cam->width, rows, hipMemcpyDefault, R.stream));
+            render_enqueue(s, R, cam, st, rows, m, L.d_out, R.stream, *P[k], stats != nullptr);
+            HIP_OK(copy_rows(d_out, L.d_out, cam->width, rows, hipMemcpyDefault, R.stream));
+            HIP_OK(hipEventRecord(L.free_ev, R.stream));  // the copy read the slot's frame
             HIP_OK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
             HIP_OK(hipEventRecord(done[k], R.stream));
         }
@@ -1724,7 +1917,7 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
         }
     } catch (...) {
         for (uint32_t k = 0; k < n; ++k)  // drain what was enqueued before the buffers go away
-            if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipStreamSynchronize(P[k]->stream); }
+            if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipDeviceSynchronize(); }
         for (hipEvent_t e : done) if (e) (void)hipEventDestroy(e);
         if (entry) (void)hipEventDestroy(entry);
         throw;
@@ -1736,8 +1929,8 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
     if (stats) *stats = acc;
 }
 
-// rs_render: every replica renders its rows into its own device frame on its own stream; the rows
-// are copied back into the caller's buffer (rows outside the call's lattice keep their values).
+// rs_render: every replica renders its rows into a frame on its own device on its own stream; the
+// rows are copied back into the caller's buffer (rows outside the call's lattice keep their values).
 void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask,
                        float* out, rs_render_stats* stats) {
     if (!out) throw Error(RS_E_INVALID, "null argument");
@@ -1748,6 +1941,7 @@ void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
     const size_t npx = (size_t)cam->width * cam->height;
     std::vector<std::unique_ptr<Pending>> P(n);
     std::vector<RowSet> rows(n);
+    std::vector<Slot*> slot(n, nullptr);
     try {
         for (uint32_t k = 0; k < n; ++k) {
             Replica& R = *s->reps[k];
@@ -1755,25 +1949,31 @@ void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
             rows[k] = replica_rows(cam, st, k, n);
             if (rows[k].count() == 0) continue;
             DeviceGuard g(R.device);
-            ensure(R.d_out, R.out_cap, npx * 4);
+            const uint32_t n_slots = s->stack_need > kStackMax ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            Slot& L = R.slots[R.next_slot % n_slots];
+            slot[k] = &L;
+            if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
+            ensure(L, L.d_out, L.out_cap, npx * 4);
             const uint8_t* m = nullptr;
             if (mask) {
-                ensure(R.d_mask, R.mask_cap, npx);
-                HIP_OK(hipMemcpyAsync(R.d_mask, mask, npx, hipMemcpyHostToDevice, R.stream));
-                m = R.d_mask;
+                ensure(L, L.d_mask, L.mask_cap, npx);
+                HIP_OK(hipMemcpyAsync(L.d_mask, mask, npx, hipMemcpyHostToDevice, R.stream));
+                m = L.d_mask;
             }
-            render_enqueue(s, R, cam, st, rows[k], m, R.d_out, R.stream, *P[k], stats != nullptr);
+            render_enqueue(s, R, cam, st, rows[k], m, L.d_out, R.stream, *P[k], stats != nullptr);
         }
         for (uint32_t k = 0; k < n; ++k) {
             if (rows[k].count() == 0) continue;
             Replica& R = *s->reps[k];
             DeviceGuard g(R.device);
-            HIP_OK(copy_rows(out, R.d_out, cam->width, rows[k], hipMemcpyDeviceToHost, R.stream));
+            HIP_OK(copy_rows(out, slot[k]->d_out, cam->width, rows[k], hipMemcpyDeviceToHost, R.stream));
+            HIP_OK(hipEventRecord(slot[k]->free_ev, R.stream));
             render_finish(s, *P[k], &acc);
+            HIP_OK(hipStreamSynchronize(R.stream));
         }
     } catch (...) {
         for (uint32_t k = 0; k < n; ++k)
-            if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipStreamSynchronize(P[k]->stream); }
+            if (P[k] && P[k]->R) { DeviceGuard g(P[k]->R->device); (void)hipDeviceSynchronize(); }
         throw;
     }
     acc.tree_arity = s->tree_arity;
@@ -1825,28 +2025,21 @@ int rs_scene_create(rs_scene** out) {
     return run([&] {
         if (!out) throw Error(RS_E_INVALID, "null");
         rs_scene* s = new rs_scene();
-        if (const char* e = std::getenv("RS_WF_CHUNK")) {
-            const unsigned long long v = std::strtoull(e, nullptr, 10);
-            if (v) s->wf_chunk = v;
-        }
-        if (const char* e = std::getenv("RS_MAX_BATCH_ITEMS")) {
-            const unsigned long long v = std::strtoull(e, nullptr, 10);
-            if (v) s->max_items_per_batch = v;
-        }
-        if (const char* e = std::getenv("RS_PHASES")) {
-            s->ph_n = 0;
-            for (const char* q = e; *q && s->ph_n < kMaxPhases;) {
-                char* end = nullptr;
-                const long v = std::strtol(q, &end, 10);
-                if (end == q || v <= 0) break;
-                s->ph_budget[s->ph_n++] = (int)v;
-                q = (*end == ',' || *end == '/') ? end + 1 : end;
-            }
-        }
-        if (const char* e = std::getenv("RS_LANES")) {
-            const unsigned long long v = std::strtoull(e, nullptr, 10);
-            if (v) s->wf_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
-        }
+#ifdef RS_DEV_KNOBS
+        // dev builds only (raysnail_amd/csrc/Makefile `dev`: libraysnail_hip_dev.so): tuning overrides
+        // for A/B runs; the shipped library reads no environment (rs_scene_set_* are the knobs)
+        auto knob = [](const char* name, unsigned long long& v) {
+            if (const char* e = std::getenv(name)) { const unsigned long long x = std::strtoull(e, nullptr, 10); if (x) v = x; }
+        };
+        unsigned long long v;
+        v = s->max_items_per_batch; knob("RS_MAX_BATCH_ITEMS", v); s->max_items_per_batch = v;
+        v = s->pool_paths; knob("RS_POOL_PATHS", v); s->pool_paths = v;
+        v = s->inject_div; knob("RS_INJECT_DIV", v); s->inject_div = (uint32_t)v;
+        v = s->wf_lanes; knob("RS_LANES", v); s->wf_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
+        v = s->stream_lanes; knob("RS_SLANES", v); s->stream_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
+        v = s->frames_in_flight; knob("RS_FRAMES", v); s->frames_in_flight = (uint32_t)std::min<unsigned long long>(v, kMaxSlots);
+        v = 0; knob("RS_EXT_SPLIT", v); s->ext_split = v != 0;
+#endif
         *out = s;
     });
 }
@@ -2050,6 +2243,23 @@ int rs_scene_set_lanes(rs_scene* s, uint32_t lanes) {
         if (!s) throw Error(RS_E_INVALID, "null argument");
         if (lanes < 1 || lanes > kMaxLanes) throw Error(RS_E_INVALID, "lanes must be 1 .. 4");
         s->wf_lanes = lanes;
+        s->stream_lanes = lanes;
+    });
+}
+int rs_scene_set_frames_in_flight(rs_scene* s, uint32_t frames) {
+    return run([&] {
+        if (!s) throw Error(RS_E_INVALID, "null argument");
+        if (frames < 1 || frames > kMaxSlots) throw Error(RS_E_INVALID, "frames in flight must be 1 .. 4");
+        s->frames_in_flight = frames;
+    });
+}
+int rs_scene_set_workspace(rs_scene* s, uint64_t max_batch_items, uint64_t pool_paths) {
+    return run([&] {
+        if (!s) throw Error(RS_E_INVALID, "null argument");
+        if (max_batch_items && max_batch_items > (1ull << 31)) throw Error(RS_E_INVALID, "max_batch_items above 2^31");
+        if (pool_paths && (pool_paths < kBlock || pool_paths > (1ull << 31))) throw Error(RS_E_INVALID, "pool_paths must be 256 .. 2^31");
+        if (max_batch_items) s->max_items_per_batch = max_batch_items;
+        if (pool_paths) s->pool_paths = pool_paths;
     });
 }
 

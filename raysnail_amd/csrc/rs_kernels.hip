@@ -33,18 +33,12 @@
 #define RS_TU_MODES 1
 #endif
 
-// the material-sorted wavefront's scene modes (rs_host.cpp: spheres, nest-0, nest-2)
-#if RS_SORTED_FLAT
-#define RS_SORTED_FLAT_CASE(...) case kSmFlat: { constexpr int SMC = kSmFlat; __VA_ARGS__; break; }
-#else
-#define RS_SORTED_FLAT_CASE(...)
-#endif
+// the streaming (material-sorted) wavefront's scene modes (rs_internal.h streaming_mode)
 #define RS_SM_SORTED_DISPATCH(sm, ...)                                     \
     do {                                                                   \
         switch (sm) {                                                      \
         case kSmNest0: { constexpr int SMC = kSmNest0; __VA_ARGS__; break; }     \
         case kSmNest2: { constexpr int SMC = kSmNest2; __VA_ARGS__; break; }     \
-        RS_SORTED_FLAT_CASE(__VA_ARGS__)                                   \
         default: { constexpr int SMC = kSmSpheres; __VA_ARGS__; break; }         \
         }                                                                  \
     } while (0)
@@ -298,21 +292,8 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, 
         return;
     }
     if (SM == kSmFlat) {  // leaf-ordered triangle copy; its `kind` field says whether entry e is one
-#ifndef RS_LTRI_GLD
-#define RS_LTRI_GLD 1
-#endif
-#if RS_LTRI_GLD
         const LTri T = ld_ltri(S.ltri, e);
-#else
-        const LTri& T = S.ltri[e];
-#endif
         if (T.kind == (double)PK_TRIANGLE) {
-#if defined(RS_EXP_NOLEAF)  // dev experiment (wrong frames): the cost of the triangle leaf tests
-            return;
-#elif defined(RS_EXP_NOLEAFMATH)  // dev experiment: loads only
-            if (T.p0[0] == 12345.0) bp = e;
-            return;
-#endif
             double t;
             if (!tri_t(T, r, tmin, best, t)) return;
             // the ray constants are recomputed here (accepted triangles only) instead of being kept
@@ -488,13 +469,7 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
     // leaves of this node (their hits only shrink the range the next node is tested with),
     // in slot order through ONE copy of the leaf test: every lane tests its k-th leaf in
     // the same pass, so a wave runs max-over-lanes leaf tests per node, not one pass per
-    // slot that any lane uses
-#ifdef RS_LEAF_PER_SLOT
-    if (l0 != INT32_MIN) RS_LEAF4(l0);
-    if (l1 != INT32_MIN) RS_LEAF4(l1);
-    if (l2 != INT32_MIN) RS_LEAF4(l2);
-    if (l3 != INT32_MIN) RS_LEAF4(l3);
-#else
+    // slot that any lane uses (one `if` per slot measured 2 % slower)
     while (true) {
         int code;
         if (l0 != INT32_MIN) { code = l0; l0 = INT32_MIN; }
@@ -504,7 +479,6 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
         else break;
         RS_LEAF4(code);
     }
-#endif
     return next;
 #undef RS_LEAF4
 #undef RS_ST_LEAF4
@@ -523,15 +497,8 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 // scenes' objects are monotone -- a later test sees a range at least as large, the closest entry wins
 // whatever the order (equal t: the first met, as before), and the winner's record needs only a range
 // end above its own t.
-#ifndef RS_LEAFQ
 #define RS_LEAFQ 8      // entries per lane (power of two, >= 8)
-#endif
-#ifndef RS_LEAFQ_THR
 #define RS_LEAFQ_THR 48  // leaf pass at >= 48/64 of the working lanes with an entry queued
-#endif
-#ifndef RS_FLAT_LEAFQ
-#define RS_FLAT_LEAFQ 1
-#endif
 template <int SM, class STK>
 __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, float tmin32, float best32, int node, int& sp,
                                            const STK& stk, int* q, int& qt) {
@@ -644,26 +611,11 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
     return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
-template <int SM, class STK>
-__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk);
-template <int SM, class STK>
-__device__ __noinline__ int traverse_call(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
-    return traverse_body<SM>(S, r, tmin, bend_out, stk);
-}
-// inlined into the kernels of every scene mode (a real call makes the kernel keep its live registers
-// in scratch across it: the nest-2 extend spilled 1.2 KB per lane); RS_GENERIC_CALL=1 keeps it a call
-// in the generic (rich) mode, measured slower there in round 3 (X1 400x400x16 54.7 vs 51.9 ms, X2
-// 300x300x64 36.9 vs 36.0 ms, bit-identical: profiles/r3/ab/generic_inline_*.txt)
+// World::hit, inlined into the kernels of every scene mode (a real call makes the kernel keep its live
+// registers in scratch across it: the nest-2 extend spilled 1.2 KB per lane; the generic mode as a
+// call measured slower in round 3, profiles/r3/ab/generic_inline_*.txt)
 template <int SM, class STK>
 __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
-#ifndef RS_GENERIC_CALL
-#define RS_GENERIC_CALL 0
-#endif
-    if constexpr (SM == kSmGeneric && RS_GENERIC_CALL) return traverse_call<SM>(S, r, tmin, bend_out, stk);
-    else return traverse_body<SM>(S, r, tmin, bend_out, stk);
-}
-template <int SM, class STK>
-__device__ __forceinline__ int traverse_body(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if (S.root < 0) return -1;
     const RayC rc = ray_consts(r);
     const RayF rf = make_rayf(r.o, rc.inv);
@@ -1063,25 +1015,13 @@ __device__ __forceinline__ void load_path(const WfSet& W, uint32_t p, Ray& r, V3
     unpack_u32x2(t.w, rng.z, rng.w);
 }
 __device__ __forceinline__ void store_path(const WfSet& W, uint32_t p, const Ray& r, const V3& T, const Rng& rng,
-                                           uint32_t item) {
+                                           uint32_t item, uint32_t level = 0) {
     D4 a, b, t;
     a.x = r.o.x; a.y = r.o.y; a.z = r.o.z; a.w = r.time;
     b.x = r.d.x; b.y = r.d.y; b.z = r.d.z; b.w = pack_u32x2(rng.x, rng.y);
     t.x = T.x; t.y = T.y; t.z = T.z; t.w = pack_u32x2(rng.z, rng.w);
     W.ray_o[p] = a; W.ray_d[p] = b; W.thr[p] = t;
-    W.item[p] = item;
-}
-
-// wave-aggregated slot allocation: one atomic per wave, flagged lanes get consecutive slots
-__device__ __forceinline__ uint32_t wave_slot(bool flag, uint32_t* counter) {
-    const unsigned long long m = __ballot(flag);
-    if (m == 0ull) return 0;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    W.tag[p] = make_uint2(item, level);
 }
 
 // Block-aggregated slot allocation for up to C independent counters: ONE returning atomic per
@@ -1152,45 +1092,31 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
     return true;
 }
 
-// Camera-ray order of the bounce-0 launches: thread i of a batch takes the sample of item
-// item0 + gen_perm(i). Within each whole sample plane of the batch the lattice pixels are visited in
-// TW x TH tiles (TW * TH = 64: one wave traces one compact pixel tile, whose camera rays take
-// nearly the same BVH path; a 64 x 1 row strip spans 8x the angle across -- bench frame 10.21 ->
-// 9.89 ms), the pixels outside the whole tiles after them in row-major order. With RS_GEN_TILE_S
-// = S > 1 a wave takes a TW x TH tile of S consecutive sample planes (TW * TH * S = 64). Pure
-// scheduling: rad[] is indexed by item, so the frame does not depend on it. A batch that is not
-// whole planes (groups of S planes) keeps the identity order.
-#ifndef RS_GEN_TILE_W
-#define RS_GEN_TILE_W 8
-#endif
-#ifndef RS_GEN_TILE_S
-#define RS_GEN_TILE_S 1
-#endif
+// Camera-ray order: the i-th camera sample a launch traces is item gen_perm(i) of its batch (whole
+// sample planes). Within each plane the lattice pixels are visited in TW x TH tiles (TW * TH = 64:
+// one wave traces one compact pixel tile, whose camera rays take nearly the same BVH path; a 64 x 1
+// row strip spans 8x the angle across -- bench frame 10.21 -> 9.89 ms), the pixels outside the whole
+// tiles after them in row-major order. Pure scheduling: rad[] is indexed by item, so the frame does
+// not depend on it. A batch that is not whole planes keeps the identity order.
 __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_t n, const PathParams& P) {
-    constexpr uint32_t S = RS_GEN_TILE_S, TW0 = RS_GEN_TILE_W ? RS_GEN_TILE_W : 1;
     // A lattice with row step k (a strong-scaled share: rows r, r + k, ...) puts TH lattice rows
     // TH * k screen rows apart: keep the tile about square on screen (step 8: 64 x 1, step 2: 16 x 4)
-    uint32_t TW = TW0, TH = 64 / (TW0 * S);
-    if (S == 1 && RS_GEN_TILE_W == 8 && P.row_step > 1) {
+    uint32_t TW = 8, TH = 8;
+    if (P.row_step > 1) {
         TH = P.row_step >= 8 ? 1u : P.row_step >= 4 ? 2u : 4u;
         TW = 64u / TH;
     }
-    const uint32_t TP = TW * TH;
     const uint32_t npl = P.n_pix_local, W = P.width;
-    if (RS_GEN_TILE_W == 0 || (item0 % npl) != 0 || (n % (npl * S)) != 0) return i;
-    const uint32_t grp = i / (npl * S);
-    uint32_t q = i - grp * (npl * S), pl, s;
+    if ((item0 % npl) != 0 || (n % npl) != 0) return i;
+    const uint32_t s = i / npl;
+    uint32_t q = i - s * npl, pl;
     const uint32_t R = npl / W, Wt = W - W % TW, Rt = R - R % TH, nt = Wt * Rt;
-    if (q < nt * S) {
+    if (q < nt) {
         const uint32_t t = q / 64u, k = q % 64u, tpr = Wt / TW;
-        const uint32_t ty = t / tpr, tx = t - ty * tpr, kk = k % TP;
-        s = k / TP;
-        pl = (ty * TH + kk / TW) * W + tx * TW + kk % TW;
+        const uint32_t ty = t / tpr, tx = t - ty * tpr;
+        pl = (ty * TH + k / TW) * W + tx * TW + k % TW;
     } else {
-        q -= nt * S;
-        const uint32_t nr = npl - nt;  // per plane: the right strip of the tiled rows, then the rows below
-        s = q / nr;
-        q -= s * nr;
+        q -= nt;  // the right strip of the tiled rows, then the rows below
         const uint32_t rw = W - Wt;
         if (q < rw * Rt) {
             const uint32_t lr = q / rw;
@@ -1199,7 +1125,7 @@ __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_
             pl = Rt * W + (q - rw * Rt);
         }
     }
-    return (grp * S + s) * npl + pl;
+    return s * npl + pl;
 }
 
 #if RS_TU_COMMON
@@ -1227,17 +1153,15 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
 }
 #endif  // RS_TU_COMMON
 
-#ifndef RS_WF_EXT_FLAT_WAVES
-#define RS_WF_EXT_FLAT_WAVES 5  // flat scenes (meshes) are traversal-latency bound: keep 5 waves/SIMD
-#endif
+// flat scenes (meshes) are traversal-latency bound: their extend keeps 5 waves/SIMD (98 -> 96 VGPRs;
+// unbounded, the mesh frame lost 18 %)
+constexpr int kWfExtFlatWaves = 5;
 template <int SM>
-__global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) void k_wf_extend(const DScene* __restrict__ Sp, WfState W, uint32_t bounce) {
+__global__ __launch_bounds__(kBlock, SM == kSmFlat ? kWfExtFlatWaves : 1) void k_wf_extend(const DScene* __restrict__ Sp, WfState W, uint32_t bounce) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const Stk stk = make_stk(S, stk_all);
-#if RS_FLAT_LEAFQ
     __shared__ int leafq[SM == kSmFlat ? RS_LEAFQ * kBlock : 1];
-#endif
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -1247,78 +1171,15 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? RS_WF_EXT_FLAT_WAVES : 1) v
             if (rich_of(SM) && S.has_media) r.key = load_rng(cur, i).medium_key();  // the segment's medium key
             double bend = RS_INF;
             int bp;
-#if RS_FLAT_LEAFQ
             if (SM == kSmFlat && S.root4 >= 0)
                 bp = traverse_flat_q<SM>(S, r, 0.0001, bend, stk, leafq + threadIdx.x);
             else
-#endif
                 bp = traverse<SM>(S, r, 0.0001, bend, stk);
             W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
         }
 #ifdef RS_TRAV_STATS
         trav_stats_flush(i < n);
 #endif
-    }
-}
-
-// ---- phased extend (flat scenes) ----
-// A lock-step wave runs the union of its lanes' traversal loops, and mesh rays differ by 10x in node
-// steps (profiles/r3/trav_stats_histogram.txt: mean 17.8, wave maximum 40.9 on the C5 mesh). Phase 0
-// runs every path of the bounce for at most `budget` 4-wide node steps; the traversals still open are
-// suspended -- next node, stack, best entry and range ends -- into a compacted continuation set, and
-// the next phase resumes them in full waves. A resumed traversal continues the same sequence of node
-// steps (best32 is a function of best and bp), so the hit is the one traverse() returns.
-template <int SM, class STK>
-__device__ __forceinline__ bool trav4_run(const DScene& S, const Ray& r, double tmin, int& node, int& sp, double& best,
-                                          double& bend, int& bp, const STK& stk, int budget) {
-    const RayC rc = ray_consts(r);
-    const RayF4 rq = make_rayf4(make_rayf(r.o, rc.inv));
-    const float tmin32 = -round_up_f(-tmin);
-    float best32 = bp >= 0 ? round_up_f(best) : __builtin_huge_valf();
-#ifdef RS_TRAV_STATS
-    int st_leaves = 0, st_witer = 0;
-#endif
-    for (int k = 0; node >= 0; ++k) {
-        if (k == budget) return false;
-        node = bvh4_step<SM>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
-    }
-    return true;
-}
-
-#ifndef RS_WF_PH_WAVES
-#define RS_WF_PH_WAVES RS_WF_EXT_FLAT_WAVES
-#endif
-template <int SM>
-__global__ __launch_bounds__(kBlock, RS_WF_PH_WAVES) void k_wf_extend_ph(const DScene* __restrict__ Sp, WfState W, uint32_t bounce,
-                                                                          ContSet in, const uint32_t* __restrict__ in_cnt,
-                                                                          ContSet out, uint32_t* __restrict__ out_cnt, int budget) {
-    const DScene& S = *Sp;
-    __shared__ int stk_all[kStackMax * kBlock];
-    const StkT<false> stk = make_stk<false>(S, stk_all);  // the host enables phases for LDS-only stacks
-    const uint32_t n = in_cnt ? *in_cnt : W.counts[bounce];
-    if (blockIdx.x * kBlock >= n) return;  // whole block past the end (uniform, before the queue barriers)
-    const WfSet& cur = W.set[bounce & 1];
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    bool open = false;
-    uint32_t i = 0;
-    int node = S.root4, sp = 0, bp = -1;
-    double best = RS_INF, bend = RS_INF;
-    if (j < n) {
-        i = j;
-        if (in_cnt) {
-            i = in.idx[j]; node = in.node[j]; sp = in.sp[j]; bp = in.bp[j]; best = in.best[j]; bend = in.bend[j];
-            for (int k = 0; k < sp; ++k) stk.lds[k * kBlock] = in.stk[(size_t)k * in.cap + j];
-        }
-        const Ray r = load_ray(cur, i);
-        open = !trav4_run<SM>(S, r, 0.0001, node, sp, best, bend, bp, stk, budget);
-        if (!open) W.hit[i] = make_double2(__longlong_as_double((long long)(bp >= 0 ? S.lprim[bp] : bp)), bend);
-    }
-    if (budget < 0) return;  // the last phase suspends nothing
-    const uint32_t slot = block_slot1(open, out_cnt);
-    if (open) {
-        out.idx[slot] = i; out.node[slot] = node; out.sp[slot] = sp; out.bp[slot] = bp;
-        out.best[slot] = best; out.bend[slot] = bend;
-        for (int k = 0; k < sp; ++k) out.stk[(size_t)k * out.cap + slot] = stk.lds[k * kBlock];
     }
 }
 
@@ -1343,7 +1204,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ 
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
             const bool ok = finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
-            item = cur.item[i];
+            item = cur.tag[i].x;
             alive = shade_step<SM>(S, ok, h, r, T, L, rng);
             if (alive && bounce + 1 >= depth) {  // depth limit
                 L = close_path(L, T);
@@ -1356,76 +1217,83 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ 
     }
 }
 
-// ---- material-sorted wavefront (spheres-only scenes) ----
-// counts layout per bounce: [0] live paths, [1 + k] paths queued for class k (k = 0 Lambertian,
-// 1 Metal, 2 DiffuseMetal, 3 Dielectric, 4 other / MixedMaterial). The class of a hit is a per-prim
-// byte (DScene::pclass) computed at commit; kClsLight marks DiffuseLight prims, whose paths end
-// inside extend like sky misses (no queue, no second gather of the path state).
+// ---- streaming material-sorted wavefront (spheres / nest-0 / nest-2 scenes) ----
+// A frame is one sequence of iterations over a pool of paths in flight. Iteration t:
+//  k_wfs_extend     World::hit for every path carried in from iteration t-1 (set t&1: light-sample
+//                   rays from the front, the rest from the back) and for the camera samples injected
+//                   at t, generated in the kernel (painter.rs:154-187, camera.rs:77-85). Sky misses and
+//                   light hits end here (their radiance is written); the rest go to the queue of their
+//                   material class.
+//  k_wfs_shade_all  every class queue in one launch: scatter (camera.rs:176-250); the survivors are
+//                   compacted into set (t+1)&1.
+// The host injects a fixed number of camera samples per iteration, so the schedule needs no read-back:
+// a sample injected at t traces its ray_color level b at iteration t + b and has finished by
+// t + depth - 1, after which its batch's radiance may be accumulated. Paths of different levels share
+// a launch; a record carries its level (WfSet::tag) for the depth limit. Every launch stays full until
+// the frame's last samples are injected: no per-bounce tail of small launches per chunk.
+// Class of a hit: a per-prim byte (DScene::pclass) computed at commit, k = 0 Lambertian, 1 Metal,
+// 2 DiffuseMetal, 3 Dielectric, 4 other / MixedMaterial / composite; kClsLight marks DiffuseLight prims,
+// whose paths end inside extend like sky misses (no queue, no second gather of the path state).
 constexpr int kClasses = kWfsClasses;
 constexpr int kClsLight = 6;
 
-#ifndef RS_EXT_MIN_WAVES
-#define RS_EXT_MIN_WAVES 1  // 5 forces <=96 VGPRs but spills; measured slower (14.5 vs 13.8 ms)
-#endif
-#ifndef RS_EXT_MIN_WAVES_N2
-#define RS_EXT_MIN_WAVES_N2 1  // nest-2 scenes (CSG of transforms: C4): 2 waves (bounce 0: 20 B spill) measured equal, 3 waves spills 288 B (C4 48.7 -> 50.4 ms)
-#endif
-#ifndef RS_EXT_MIN_WAVES_N0
-#define RS_EXT_MIN_WAVES_N0 4  // nest-0 scenes (boxes, quadrics: C2): 129 -> 128 VGPRs, example.sdl 10.8 -> 10.3 ms
-#endif
-// GEN = bounce 0 fused with ray generation: thread i owns camera sample item0 + i, traverses it
-// straight from registers, and only the paths that go on to shading are written (at index i, with
-// T = 1 and L = 0 implied for the bounce-0 shade kernels). (Writing only the hit and regenerating the
-// camera ray in the bounce-0 shade kernels instead cut 0.27 GB of HBM traffic per launch but made the
-// bench frame slower, 10.20 -> 10.26 ms: the stores are not what bounds this kernel.)
-#ifndef RS_SPH_LEAFQ
-#define RS_SPH_LEAFQ 0  // spheres scenes: queued-leaf traversal (traverse_flat_q) on bounces >= 1 (1) or all (2)
-#endif
-#ifndef RS_EXT_GEN_MIN_WAVES
-#define RS_EXT_GEN_MIN_WAVES 4  // the spheres-mode bounce-0 (camera ray) extend: 144 -> 128 VGPRs, bench frame 7.86 -> 7.63 ms
-#endif
-template <bool GEN, int SM, bool OVF>
-__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM == kSmNest0 ? RS_EXT_MIN_WAVES_N0 : GEN ? RS_EXT_GEN_MIN_WAVES : RS_EXT_MIN_WAVES) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
-                                                      uint32_t bounce, uint32_t stride, uint64_t n_items,
-                                                      double* __restrict__ rad, DCamera C, PathParams P,
-                                                      uint64_t item0, uint32_t n_gen) {
+// waves/SIMD the extend is bounded to: spheres and nest-0 scenes 4 (128 VGPRs; the spheres-mode
+// camera-ray extend 144 -> 128 VGPRs: bench frame 7.86 -> 7.63 ms; nest-0 129 -> 128: example.sdl
+// 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 2 (unbounded, the camera part took
+// 2 AGPRs beyond 256 VGPRs: one wave per SIMD; 3 waves spilled 288 B)
+constexpr int ext_min_waves(int sm) { return sm == kSmNest2 ? 2 : 4; }
+// PART (rs_internal.h): kExtAll -- the carried paths and the injected camera samples in one launch;
+// kExtCarried / kExtCamera -- one of the two (an iteration then takes two launches): where the merged
+// kernel needs more registers than either alone (nest-2: 256 VGPRs + 2 AGPRs, one wave per SIMD,
+// against two waves for each part)
+template <int SM, bool OVF, int PART>
+__global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W,
+                                                                          uint32_t* const* __restrict__ queues, uint32_t it,
+                                                                          double* __restrict__ rad, DCamera C, PathParams P,
+                                                                          InjParams I) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     __shared__ int stk_all[kStackMax * kBlock];
     const StkT<OVF> stk = make_stk<OVF>(S, stk_all);
-#if RS_SPH_LEAFQ
-    __shared__ int leafq[SM == kSmSpheres ? RS_LEAFQ * kBlock : 1];
-#endif
-    uint32_t* cnt = W.counts + (size_t)bounce * stride;
-    const uint32_t nf = GEN ? 0u : cnt[cix(kCntFront)];
-    const uint32_t n = GEN ? n_gen : nf + cnt[cix(kCntBack)];
-    if (!GEN && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n;  // live paths at this bounce (stats)
-    const WfSet& cur = W.set[bounce & 1];
+    uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
+    const uint32_t nf = cnt[cix(kCntFront)];
+    const uint32_t n_old = PART == kExtCamera ? 0u : nf + cnt[cix(kCntBack)];
+    const uint32_t n = n_old + (PART == kExtCarried ? 0u : I.n_new);
+    if (PART != kExtCamera && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n_old;  // paths carried in (stats)
+    const WfSet& cur = W.set[it & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        // thread -> record: the front run [0, nf), then the back run from the set's end down
+        // thread -> record: the front run [0, nf), the back run from the set's end down, then the
+        // injected camera samples, whose records follow the front run
         const uint32_t j = base + threadIdx.x;
-        const uint32_t i = (GEN || j < nf) ? j : W.cap - 1u - (j - nf);
+        const bool gen = PART == kExtCamera || (PART == kExtAll && j >= n_old);
+        const uint32_t i = gen ? nf + (j - n_old) : j < nf ? j : W.cap - 1u - (j - nf);
         int cls = -1;
         bool live = false;
         if (j < n) {
             Ray r;
             Rng rng;
             uint32_t item = 0;
-            if (GEN) {
-                item = (uint32_t)(item0 + gen_perm(i, item0, n_gen, P));
-                live = camera_sample(C, P, item, r, rng);
-                if (!live) { rad[item] = 0.0; rad[n_items + item] = 0.0; rad[2 * n_items + item] = 0.0; }
+            if (gen) {
+                uint32_t jb = I.jb0 + (j - n_old), nb = I.nb0;
+                uint64_t g0 = I.g0;
+                item = I.rad0;
+                if (jb >= I.nb0) { jb -= I.nb0; nb = I.nb1; g0 = I.g1; item = I.rad1; }
+                const uint32_t perm = gen_perm(jb, 0, nb, P);
+                item += perm;
+                live = camera_sample(C, P, g0 + perm, r, rng);
+                if (!live) {
+                    rad[item] = 0.0; rad[I.ring + item] = 0.0; rad[2 * I.ring + item] = 0.0;
+                } else {
+                    // the record is written before the traversal (most camera samples go on to
+                    // shading), so the RNG state is not held in registers across it
+                    store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
+                }
             } else {
                 r = load_ray(cur, i);
                 live = true;
             }
             if (live) {
                 double bend = RS_INF;
-#if RS_SPH_LEAFQ
-                const int bp = (SM == kSmSpheres && (!GEN || RS_SPH_LEAFQ > 1)) ? traverse_flat_q<SM>(S, r, 0.0001, bend, stk, leafq + threadIdx.x)
-                                                  : traverse<SM>(S, r, 0.0001, bend, stk);
-#else
                 const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
-#endif
                 V3 add;
                 bool done = true;
                 if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
@@ -1457,112 +1325,57 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? RS_EXT_MIN_WAVES_N2 : SM =
                         cls = -1;
                     } else {
                         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-                        if (GEN) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item);
                         done = false;
                     }
                 }
                 if (done) {  // 0 + T * add: the path's radiance so far is 0 (WfSet)
-                    D4 t4;
-                    if (GEN) {
-                        t4.x = t4.y = t4.z = 1.0;
-                    } else {
-                        t4 = cur.thr[i]; item = cur.item[i];
-                    }
+                    // (a camera sample's record was written by this thread before the traversal: T = 1)
+                    const D4 t4 = cur.thr[i];
+                    item = cur.tag[i].x;
                     rad[item] = 0.0 + t4.x * add.x;
-                    rad[n_items + item] = 0.0 + t4.y * add.y;
-                    rad[2 * n_items + item] = 0.0 + t4.z * add.z;
+                    rad[I.ring + item] = 0.0 + t4.y * add.y;
+                    rad[2 * I.ring + item] = 0.0 + t4.z * add.z;
                 }
             }
         }
 #ifdef RS_TRAV_STATS
         trav_stats_flush(live);
 #endif
-        // sub-queue of this batch of 256 paths (bounded by WfState::qsub, rs_internal.h)
-        const uint32_t g = (base / kBlock) % kQSub;
-        uint32_t* const cs[kClasses] = {&cnt[cix(1, g)], &cnt[cix(2, g)], &cnt[cix(3, g)], &cnt[cix(4, g)], &cnt[cix(5, g)]};
-        // bounce 0 also counts its live camera samples (segments, stats) in the same block reduction
-        // (the live-sample count goes to one of kStatLines counters on their own lines, by block: a
-        // single word takes ~88 atomics/us, and one per block of a 25.6 M-sample launch kept the
-        // bounce-0 kernel near that ceiling -- 1.14 ms for an empty launch, 0.10 ms spread)
-        const uint32_t slot = block_slot<kClasses>(cls, cs, live, GEN ? &cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))] : nullptr);
-        if (cls >= 0) queues[cls][g * W.qsub + slot] = i;
+        // the iteration's live segments are counted in the same block reduction, on one of kStatLines
+        // counters by block (one returning-free atomic per block on a single word capped an empty
+        // camera-ray launch at ~88 atomics/us: 1.14 ms for 25.6 M samples, 0.10 ms spread)
+        uint32_t* const cs[kClasses] = {&cnt[cix(1)], &cnt[cix(2)], &cnt[cix(3)], &cnt[cix(4)], &cnt[cix(5)]};
+        const uint32_t slot = block_slot<kClasses>(cls, cs, live, &cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))]);
+        if (cls >= 0) queues[cls][slot] = i;
     }
 }
 
-// Block-local reordering by a small key (0..2): lane p of the block is given the item of the p-th
-// lane in (key, wave, lane) order, so each wave holds items of one key except at key boundaries.
-// Pure scheduling: every item is still processed exactly once, by some lane of this block.
-__device__ __forceinline__ uint32_t block_sort3(int key, uint32_t j) {
-    __shared__ uint32_t wcnt[3][kBlock / 64];
-    __shared__ uint32_t perm[kBlock];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long mine = 0ull;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const unsigned long long m = __ballot(key == k);
-        if (key == k) mine = m;
-        if (lane == 0) wcnt[k][wave] = (uint32_t)__popcll(m);
-    }
-    __syncthreads();
-    uint32_t off = 0;
-    for (int k = 0; k < 3; ++k)
-        for (int w = 0; w < kBlock / 64; ++w) {
-            const uint32_t c = wcnt[k][w];
-            if (k < key || (k == key && w < wave)) off += c;
-        }
-    perm[off + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull))] = j;
-    __syncthreads();
-    const uint32_t r = perm[threadIdx.x];
-    __syncthreads();  // wcnt / perm are reused by the next call
-    return r;
-}
-
-#ifndef RS_LAMB_MIN_WAVES
-#define RS_LAMB_MIN_WAVES 4  // 130 -> 128 VGPRs (4 waves/SIMD, 12 B spill): 10.01 -> 9.94 ms bench frame
-#endif
-// One batch of 256 queued paths of material class `cls` (entries base .. base + 255 of the class
-// queue, the concatenation of its kQSub sub-queues with lengths qn[], n in all): finish the hit
-// record, scatter, write the radiance of paths that end and append the survivors to the next set.
-// Must be called by every thread of the block (block_slot).
+// One batch of 256 queued paths of material class KIND (-1: the generic material switch; entries
+// base .. base + 255 of a queue of n): finish the hit record, scatter, write the radiance of paths that
+// end and append the survivors to the next set. Must be called by every thread of the block (block_slot).
 template <int KIND, int SM>
 __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const uint32_t* __restrict__ queue,
-                                                const uint32_t* qn, uint32_t n, uint32_t base, uint32_t bounce,
-                                                uint32_t* cnt_next, uint32_t depth, uint64_t n_items,
-                                                double* __restrict__ rad) {
-    const WfSet& cur = W.set[bounce & 1];
-    const WfSet& nxt = W.set[(bounce + 1) & 1];
-    uint32_t j = base + threadIdx.x;
-#ifdef RS_BRANCH_SORT  // measured: no gain on the bench frame (11.97 vs 11.80 ms)
-    if (KIND == RS_MAT_LAMBERTIAN || KIND == RS_MAT_DIFFUSE_METAL) {
-        // camera.rs:196-218 takes the light branch or the BSDF branch on the path's next draw
-        // (for these materials the first draw of the bounce); both are long, so peek that draw
-        // and group the block's paths by branch -- each wave then runs one branch
-        int key = 2;
-        if (j < n) {
-            Rng pk = load_rng(cur, queue[j]);
-            key = pk.gen() < 0.5 ? 0 : 1;
-        }
-        j = block_sort3(key, j);
-    }
-#endif
+                                                uint32_t n, uint32_t base, uint32_t it, uint32_t* cnt_next, uint32_t depth,
+                                                uint64_t ring, double* __restrict__ rad) {
+    const WfSet& cur = W.set[it & 1];
+    const WfSet& nxt = W.set[(it + 1) & 1];
+    const uint32_t j = base + threadIdx.x;
     bool alive = false;
     int light_ray = 0;
     Ray r;
     V3 T;
     Rng rng;
-    uint32_t item = 0;
+    uint32_t item = 0, lvl = 0;
     if (j < n) {
-        uint32_t g = 0, off = j;
-#pragma unroll
-        for (uint32_t k = 0; k + 1 < kQSub; ++k)
-            if (g == k && off >= qn[k]) { off -= qn[k]; g = k + 1; }
-        const uint32_t i = queue[g * W.qsub + off];
+        const uint32_t i = queue[j];
         load_path(cur, i, r, T, rng);
         const double2 hb = W.hit[i];
         const int bp = (int)__double_as_longlong(hb.x);
         Hit h;
         finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
-        item = cur.item[i];
+        const uint2 tg = cur.tag[i];
+        item = tg.x;
+        lvl = tg.y;
         const int mi = h.mat >= 0 ? h.mat : S.default_mat;
         const DMaterial& M0 = S.mats[mi];
         bool cont;
@@ -1573,76 +1386,55 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
             // None (camera.rs:172-176, 250), 0 + T * e as in shade_step
             const V3 e = emission<0>(S, M0, h);
             const V3 L = v3(0.0, 0.0, 0.0) + v3(T.x * e.x, T.y * e.y, T.z * e.z);
-            rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
+            rad[item] = L.x; rad[ring + item] = L.y; rad[2 * ring + item] = L.z;
             cont = false;
             item = ~0u;  // radiance written
         } else {
             int ms = mi;
-            for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {
+            for (int k = 0; k < 16 && S.mats[ms].kind == RS_MAT_MIXED; ++k) {  // mixed_material.rs:43-50
                 const DMaterial& X = S.mats[ms];
                 ms = ((double)rng.next_u32() < 4294967295.0 * X.mix_p) ? X.mix_a : X.mix_b;
             }
             cont = shade_surface<-1, SM>(S, h, M0, S.mats[ms], r, T, rng, &light_ray);
         }
-        alive = cont && (bounce + 1 < depth);
+        alive = cont && (lvl + 1 < depth);  // the depth limit of ray_color (camera.rs:161)
         if (!alive && item != ~0u) {  // absorbed or depth limit: no emission term
             const V3 L = close_path(v3(0.0, 0.0, 0.0), T);
-            rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z;
+            rad[item] = L.x; rad[ring + item] = L.y; rad[2 * ring + item] = L.z;
         }
     }
     // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
     // the front, the rest from the back: the next extend's waves then trace rays of one kind
     uint32_t* const gc[2] = {&cnt_next[cix(kCntBack)], &cnt_next[cix(kCntFront)]};
     const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
-    if (alive) store_path(nxt, light_ray ? slot : W.cap - 1u - slot, r, T, rng, item);
+    if (alive) {
+        const uint32_t p = light_ray ? slot : W.cap - 1u - slot;
+        store_path(nxt, p, r, T, rng, item, lvl + 1u);
+    }
 }
 
-// the class queue's sub-queue lengths and their sum
-__device__ __forceinline__ uint32_t class_queue_len(const uint32_t* cnt, int cls, uint32_t* qn) {
-    uint32_t n = 0;
-#pragma unroll
-    for (uint32_t g = 0; g < kQSub; ++g) { qn[g] = cnt[cix(1 + cls, g)]; n += qn[g]; }
-    return n;
-}
-
-template <int KIND, int SM>
-__global__ __launch_bounds__(kBlock, (KIND == RS_MAT_LAMBERTIAN && SM != kSmNest2) ? RS_LAMB_MIN_WAVES : 1) void k_wfs_shade(const DScene* __restrict__ Sp, WfState W, const uint32_t* __restrict__ queue,
-                                                     int cls, uint32_t bounce, uint32_t stride, uint32_t depth,
-                                                     uint64_t n_items, double* __restrict__ rad) {
-    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
-    const uint32_t* cnt = W.counts + (size_t)bounce * stride;
-    uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
-    uint32_t qn[kQSub];
-    const uint32_t n = class_queue_len(cnt, cls, qn);
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock)
-        wfs_shade_batch<KIND, SM>(S, W, queue, qn, n, base, bounce, cnt_next, depth, n_items, rad);
-}
-
-// The material classes of a bounce in ONE launch (rs_host.cpp RS_SHADE_MERGED): the grid walks the
-// concatenation of the class queues' 256-path batches (class 0's, then class 1's, ...); a block's
-// class is uniform, so each batch runs its class's specialised code. One launch per bounce instead
-// of one per class removes the per-class launch tails (the small classes' queues take 5-50 us each
-// however short they are), which is what bounds the per-GPU share of a strong-scaled frame.
-// Classes kShadeAllFirst .. 3 (RS_SHADE_MERGED 1: Lambertian too; 2: Lambertian keeps its own
-// 4-wave kernel); class 4 (MixedMaterial / other, the generic material switch and the most
-// registers) keeps its own launch when a scene has it.
-constexpr int kShadeAllLast = 3;
-#ifndef RS_SHADE_ALL_WAVES
-#define RS_SHADE_ALL_WAVES 3  // 171 -> 168 VGPRs, 3 waves/SIMD (nest-2 unbounded: 76 VGPRs would spill, C4 -21 %)
-#endif
-template <int SM>
-__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? 1 : RS_SHADE_ALL_WAVES) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W, uint32_t* const* __restrict__ queues,
-                                                                              uint32_t class_mask, uint32_t bounce, uint32_t stride,
-                                                                              uint32_t depth, uint64_t n_items, double* __restrict__ rad) {
+// Every material class of an iteration in ONE launch: the grid walks the concatenation of the class
+// queues' 256-path batches (class 0's, then class 1's, ...); a block's class is uniform, so each batch
+// runs its class's specialised code. One launch per iteration instead of one per class removes the
+// per-class launch tails (the small classes' queues take 5-50 us each however short they are).
+// G4: the scene has class-4 prims (the generic material switch, composite objects), compiled in only
+// then (it sets the kernel's register count).
+template <int SM, bool G4>
+__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
+                                                                                   uint32_t* const* __restrict__ queues,
+                                                                                   uint32_t class_mask, uint32_t it,
+                                                                                   uint32_t depth, uint64_t ring,
+                                                                                   double* __restrict__ rad) {
+    // (3 waves: 171 -> 168 VGPRs; at 4 waves it spilled 156 B, +6 %; nest-2 bounded at 3 spilled: C4 -21 %)
     const DScene& S = *Sp;
-    const uint32_t* cnt = W.counts + (size_t)bounce * stride;
-    uint32_t* cnt_next = W.counts + (size_t)(bounce + 1) * stride;
-    constexpr int NC = kShadeAllLast + 1;
-    uint32_t qn[NC][kQSub], n[NC], first[NC + 1];
+    const uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
+    uint32_t* cnt_next = W.counts + (size_t)(it + 1) * kWfsStride;
+    constexpr int NC = G4 ? 5 : 4;
+    uint32_t n[NC], first[NC + 1];
     first[0] = 0;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-        n[k] = (k >= kShadeAllFirst && (class_mask >> k & 1u)) ? class_queue_len(cnt, k, qn[k]) : 0u;
+        n[k] = (class_mask >> k & 1u) ? cnt[cix(1 + k)] : 0u;
         first[k + 1] = first[k] + (n[k] + kBlock - 1) / kBlock;
     }
     for (uint32_t v = blockIdx.x; v < first[NC]; v += gridDim.x) {
@@ -1650,24 +1442,27 @@ __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? 1 : RS_SHADE_ALL_WAVES) vo
 #pragma unroll
         for (int c = 1; c < NC; ++c) k += v >= first[c] ? 1 : 0;
         const uint32_t base = (v - first[k]) * kBlock;
-        if (kShadeAllFirst == 0 && k == 0)
-            wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], qn[0], n[0], base, bounce, cnt_next, depth, n_items, rad);
+        if (k == 0)
+            wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], n[0], base, it, cnt_next, depth, ring, rad);
         else if (k == 1)
-            wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], qn[1], n[1], base, bounce, cnt_next, depth, n_items, rad);
+            wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], n[1], base, it, cnt_next, depth, ring, rad);
         else if (k == 2)
-            wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], qn[2], n[2], base, bounce, cnt_next, depth, n_items, rad);
+            wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], n[2], base, it, cnt_next, depth, ring, rad);
+        else if (k == 3 || !G4)
+            wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], n[3], base, it, cnt_next, depth, ring, rad);
         else
-            wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], qn[3], n[3], base, bounce, cnt_next, depth, n_items, rad);
+            wfs_shade_batch<-1, SM>(S, W, queues[NC - 1], n[NC - 1], base, it, cnt_next, depth, ring, rad);
     }
 }
+
 
 #if RS_TU_COMMON
 // painter.rs:167-179: a pixel's sum over its samples, in sample order. One thread per (pixel,
 // channel), the batch's samples read 16 at a time (the adds stay in order): a strong-scaled share of
 // a frame has few pixels, and a thread per pixel looping over 3 x N dependent loads left the kernel
 // latency-bound (80 us for the N = 8 share of the bench frame).
-__global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict__ rad, double* __restrict__ acc, uint32_t n_pix,
-                                                      uint32_t n_samp, int first, int last, FinalParams P,
+__global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict__ rad, uint64_t stride, double* __restrict__ acc,
+                                                      uint32_t n_pix, uint32_t n_samp, int first, int last, FinalParams P,
                                                       float* __restrict__ out, uint32_t* __restrict__ zero, uint32_t n_zero) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     // the frame's queue counters, read by no kernel after this one: reset for the next frame
@@ -1675,9 +1470,8 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict_
     for (uint64_t z = t; z < n_zero; z += (uint64_t)gridDim.x * kBlock) zero[z] = 0u;
     if (t >= 3ull * n_pix) return;
     const uint32_t c = (uint32_t)(t / n_pix), p = (uint32_t)(t - (uint64_t)c * n_pix);
-    const uint64_t n_items = (uint64_t)n_pix * n_samp;
     double a = first ? 0.0 : acc[(uint64_t)c * n_pix + p];
-    const double* rc = rad + (uint64_t)c * n_items + p;
+    const double* rc = rad + (uint64_t)c * stride + p;
     uint32_t s = 0;
     for (; s + 16 <= n_samp; s += 16) {
         double v[16];
@@ -1837,22 +1631,14 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
                              double* rad, uint32_t blocks, hipStream_t st), (s, w, bounce, depth, n_items, rad, blocks, st)) \
     X(hipError_t, wf_occupancy, (int* e, int* sh), (e, sh))
 #define RS_SORTED_LAUNCHERS(X)                                                                                 \
-    X(hipError_t, wfs_extend, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce,   \
-                               uint32_t stride, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st,   \
-                               hipEvent_t ev0, hipEvent_t ev1),                                                \
-      (s, w, queues, bounce, stride, n_items, rad, blocks, st, ev0, ev1))                                      \
-    X(hipError_t, wfs_gen_extend, (const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,  \
-                                   uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad, \
-                                   uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1),              \
-      (s, c, p, w, queues, stride, item0, n, rad, blocks, st, ev0, ev1))                                       \
+    X(hipError_t, wfs_extend, (const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,       \
+                               uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, \
+                               int part, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1),                        \
+      (s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1))                                                  \
     X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, \
-                                  uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,  \
-                                  uint32_t blocks, hipStream_t st),                                             \
-      (s, w, queues, class_mask, bounce, stride, depth, n_items, rad, blocks, st))                             \
-    X(hipError_t, wfs_shade, (const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce, \
-                              uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks,    \
-                              hipStream_t st),                                                                  \
-      (s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st))
+                                  uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks,       \
+                                  hipStream_t st),                                                              \
+      (s, w, queues, class_mask, it, depth, ring, rad, blocks, st))
 #define RS_DECLARE_SM(R, NAME, PARAMS, ARGS) template <int SMC> R NAME##_sm PARAMS;
 RS_SM_LAUNCHERS(RS_DECLARE_SM)
 RS_SORTED_LAUNCHERS(RS_DECLARE_SM)
@@ -1900,77 +1686,50 @@ hipError_t wf_occupancy_sm(int* e, int* sh) {
 // the LDS-only traversal stack (StkT<false>) where the tree allows it; spheres mode only (the other
 // modes keep one instantiation each: compile time)
 [[maybe_unused]] static inline bool lds_only_stack(const SceneRef& s) { return s.host->stack_need + 3 <= kStackMax; }
-template <bool GEN, int SMC, class... A>
-static void ext_launch(const SceneRef& s, uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, A... args) {
-    if constexpr (SMC == kSmSpheres) {
-        if (lds_only_stack(s)) {
-            hipExtLaunchKernelGGL((k_wfs_extend<GEN, SMC, false>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, args...);
-            return;
-        }
-    }
-    hipExtLaunchKernelGGL((k_wfs_extend<GEN, SMC, true>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, args...);
-}
 
 template <int SMC>
-hipError_t wfs_extend_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
-                         uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    ext_launch<false, SMC>(s, blocks, st, ev0, ev1, s.dev, w, queues, bounce, stride, n_items, rad, DCamera{}, PathParams{},
-                           0ull, 0u);
-    return hipGetLastError();
-}
-
-template <int SMC>
-hipError_t wfs_gen_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
-                             uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
-                             uint32_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w, uint32_t* const* queues,
+                         uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, int part, hipStream_t st,
+                         hipEvent_t ev0, hipEvent_t ev1) {
     if (!blocks) return hipSuccess;
-    ext_launch<true, SMC>(s, blocks, st, ev0, ev1, s.dev, w, queues, 0u, stride, p.n_items, rad, c, p, item0, n);
-    return hipGetLastError();
-}
-
-template <int SMC>
-hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
-                            uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,
-                            uint32_t blocks, hipStream_t st) {
-    if (!blocks) return hipSuccess;
-    hipLaunchKernelGGL((k_wfs_shade_all<SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues, class_mask, bounce,
-                       stride, depth, n_items, rad);
-    return hipGetLastError();
-}
-
-template <int SMC>
-hipError_t wfs_shade_sm(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
-                        uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, hipStream_t st) {
-#define RS_SHADE_LAUNCH(KIND) \
-    hipLaunchKernelGGL((k_wfs_shade<KIND, SMC>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queue, cls, bounce, \
-                       stride, depth, n_items, rad)
-    switch (cls) {
-    case 0: RS_SHADE_LAUNCH(RS_MAT_LAMBERTIAN); break;
-    case 1: RS_SHADE_LAUNCH(RS_MAT_METAL); break;
-    case 2: RS_SHADE_LAUNCH(RS_MAT_DIFFUSE_METAL); break;
-    case 3: RS_SHADE_LAUNCH(RS_MAT_DIELECTRIC); break;
-    default: RS_SHADE_LAUNCH(-1); break;
+#define RS_EXT_LAUNCH(OVF, PART)                                                                                   \
+    hipExtLaunchKernelGGL((k_wfs_extend<SMC, OVF, PART>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, s.dev, w, \
+                          queues, it, rad, c, p, inj)
+    if constexpr (SMC == kSmNest2) {  // split launches only (ext_split)
+        if (part == kExtCamera) RS_EXT_LAUNCH(true, kExtCamera);
+        else RS_EXT_LAUNCH(true, kExtCarried);
+    } else if constexpr (SMC == kSmSpheres) {
+        const bool lds = lds_only_stack(s);
+        if (part == kExtAll) { if (lds) RS_EXT_LAUNCH(false, kExtAll); else RS_EXT_LAUNCH(true, kExtAll); }
+        else if (part == kExtCamera) { if (lds) RS_EXT_LAUNCH(false, kExtCamera); else RS_EXT_LAUNCH(true, kExtCamera); }
+        else { if (lds) RS_EXT_LAUNCH(false, kExtCarried); else RS_EXT_LAUNCH(true, kExtCarried); }
+    } else {
+        if (part == kExtAll) RS_EXT_LAUNCH(true, kExtAll);
+        else if (part == kExtCamera) RS_EXT_LAUNCH(true, kExtCamera);
+        else RS_EXT_LAUNCH(true, kExtCarried);
     }
-#undef RS_SHADE_LAUNCH
+#undef RS_EXT_LAUNCH
+    return hipGetLastError();
+}
+
+template <int SMC>
+hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, uint32_t it,
+                            uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, hipStream_t st) {
+    if (!blocks) return hipSuccess;
+    if (class_mask & (1u << 4))
+        hipLaunchKernelGGL((k_wfs_shade_all<SMC, true>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues, class_mask, it,
+                           depth, ring, rad);
+    else
+        hipLaunchKernelGGL((k_wfs_shade_all<SMC, false>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues, class_mask, it,
+                           depth, ring, rad);
     return hipGetLastError();
 }
 #endif  // RS_TU_MODES
 
-#if !defined(RS_TU) || RS_TU == 2  // flat scenes: the phased extend
-hipError_t launch_wf_extend_ph(const SceneRef& s, const WfState& w, uint32_t bounce, const ContSet& in,
-                               const uint32_t* in_cnt, const ContSet& out, uint32_t* out_cnt, int budget, uint32_t blocks,
-                               hipStream_t st) {
-    if (!blocks) return hipSuccess;
-    hipLaunchKernelGGL(k_wf_extend_ph<kSmFlat>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, in, in_cnt, out, out_cnt,
-                       budget);
-    return hipGetLastError();
-}
-#endif
-
 #if defined(RS_TU) && RS_TU >= 0  // this unit's mode
 #define RS_INSTANTIATE_SM(R, NAME, PARAMS, ARGS) template R NAME##_sm<RS_TU> PARAMS;
 RS_SM_LAUNCHERS(RS_INSTANTIATE_SM)
-#if RS_TU == 1 || RS_TU == 3 || RS_TU == 4 || (RS_SORTED_FLAT && RS_TU == 2)  // the sorted-wavefront modes
+#if RS_TU == 1 || RS_TU == 3 || RS_TU == 4  // the streaming-wavefront modes
 RS_SORTED_LAUNCHERS(RS_INSTANTIATE_SM)
 #endif
 #endif
@@ -2014,32 +1773,17 @@ hipError_t wf_occupancy(int sm, int* e, int* sh) {
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_wfs_extend(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t bounce, uint32_t stride,
-                            uint64_t n_items, double* rad, uint32_t blocks, int sm, hipStream_t st, hipEvent_t ev0,
-                            hipEvent_t ev1) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_extend_sm<SMC>(s, w, queues, bounce, stride, n_items, rad, blocks, st, ev0, ev1));
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_wfs_gen_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
-                                uint32_t* const* queues, uint32_t stride, uint64_t item0, uint32_t n, double* rad,
-                                uint32_t blocks, int sm, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_gen_extend_sm<SMC>(s, c, p, w, queues, stride, item0, n, rad, blocks, st, ev0, ev1));
+hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
+                             uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
+                             int part, int sm, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    RS_SM_SORTED_DISPATCH(sm, return wfs_extend_sm<SMC>(s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1));
     return hipErrorInvalidValue;
 }
 
 hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
-                                uint32_t bounce, uint32_t stride, uint32_t depth, uint64_t n_items, double* rad,
-                                uint32_t blocks, int sm, hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, bounce, stride, depth, n_items, rad,
-                                                           blocks, st));
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_wfs_shade(const SceneRef& s, const WfState& w, const uint32_t* queue, int cls, uint32_t bounce,
-                           uint32_t stride, uint32_t depth, uint64_t n_items, double* rad, uint32_t blocks, int sm,
-                           hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_sm<SMC>(s, w, queue, cls, bounce, stride, depth, n_items, rad, blocks, st));
+                                uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, int sm,
+                                hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, it, depth, ring, rad, blocks, st));
     return hipErrorInvalidValue;
 }
 
@@ -2069,12 +1813,12 @@ hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, d
     return hipGetLastError();
 }
 
-hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch, int first_batch,
-                             int last_batch, const FinalParams& p, float* out_rgba, uint32_t* zero, uint32_t n_zero,
-                             hipStream_t st) {
+hipError_t launch_accumulate(const double* rad, uint64_t stride, double* acc, uint32_t n_pix, uint32_t n_samp_batch,
+                             int first_batch, int last_batch, const FinalParams& p, float* out_rgba, uint32_t* zero,
+                             uint32_t n_zero, hipStream_t st) {
     const uint32_t blocks = (uint32_t)((3ull * n_pix + kBlock - 1) / kBlock);
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kBlock), 0, st, rad, acc, n_pix, n_samp_batch, first_batch,
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kBlock), 0, st, rad, stride, acc, n_pix, n_samp_batch, first_batch,
                        last_batch, p, out_rgba, zero, n_zero);
     return hipGetLastError();
 }

@@ -43,7 +43,8 @@ def gather_rows(frame: torch.Tensor, rank: int, world: int, dst: int = 0):
 
     Per frame: one strided copy (pack), the gather straight into a (world, per, W, 4) buffer, and on
     dst one permuted copy into a (per * world, W, 4) frame whose rows p * world + r are rank r's p-th
-    row (the rows past H are padding). Buffers are kept across frames."""
+    row (the rows past H are padding). The staging buffers of the last frame shape are kept across
+    frames; the returned frame is a fresh tensor (a caller may keep it, e.g. to combine passes)."""
     H = frame.shape[0]
     if world == 1:
         return frame
@@ -54,14 +55,15 @@ def gather_rows(frame: torch.Tensor, rank: int, world: int, dst: int = 0):
     if buf is None:
         packed = torch.zeros((per,) + rest, dtype=frame.dtype, device=frame.device)
         allp = torch.empty((world, per) + rest, dtype=frame.dtype, device=frame.device) if rank == dst else None
-        full = torch.empty((per * world,) + rest, dtype=frame.dtype, device=frame.device) if rank == dst else None
-        _ROWBUF[key] = buf = (packed, allp, full)
-    packed, allp, full = buf
+        _ROWBUF.clear()  # one shape's buffers at a time
+        _ROWBUF[key] = buf = (packed, allp)
+    packed, allp = buf
     n = rows_of(rank, world, H)
     packed[:n].copy_(frame[rank::world])
     dist.gather(packed, list(allp.unbind(0)) if rank == dst else None, dst=dst)
     if rank != dst:
         return None
+    full = torch.empty((per * world,) + rest, dtype=frame.dtype, device=frame.device)
     full.view((per, world) + rest).copy_(allp.transpose(0, 1))
     return full[:H]
 

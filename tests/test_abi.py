@@ -24,7 +24,7 @@ def test_header_lists_all_exports():
 def test_library_exports_every_declared_symbol(hip_lib):
     for name in header_symbols():
         assert hasattr(hip_lib, name), name
-    assert hip_lib.rs_abi_version() == 4
+    assert hip_lib.rs_abi_version() == 5
 
 
 def _scene(lib):

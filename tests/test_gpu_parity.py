@@ -142,13 +142,14 @@ def test_determinism_batching_and_rows(gpu, monkeypatch, mode):
     b = photo.shot(None, world)
     assert np.array_equal(a, b)
     # tiny batches: samples split over many launches, accumulated in sample order
-    monkeypatch.setenv("RS_MAX_BATCH_ITEMS", "5000")
     cam2, world2, _, _ = scenes.rtow_13_1(120, 75)
+    world2.device_scene().set_workspace(max_batch_items=5000)
     c = cam2.take_photo().samples(9).depth(8).seed(3).mode(mode).shot(None, world2)
     assert np.array_equal(a, c)
-    # tiny wavefront chunks: many chunks per batch
-    monkeypatch.setenv("RS_WF_CHUNK", "3000")
+    # tiny path sets: many chunks per batch (bounce-synchronous) / a small streaming pool with many
+    # injections per batch
     cam3, world3, _, _ = scenes.rtow_13_1(120, 75)
+    world3.device_scene().set_workspace(pool_paths=3000)
     d = cam3.take_photo().samples(9).depth(8).seed(3).mode(mode).shot(None, world3)
     assert np.array_equal(a, d)
     # rows interleaved over 3 "ranks" into one buffer == full frame (painter.rs:248)
@@ -277,8 +278,8 @@ def test_obj_mesh_scene_matches_oracle(gpu, tmp_path):
 
 def test_rich_scene_deep_paths_and_batching(gpu, monkeypatch):
     """Media / Perlin / Image scenes at depth 50 with tiny wavefront chunks: still bit-identical."""
-    monkeypatch.setenv("RS_WF_CHUNK", "2000")
     cam, world = scenes.materials_scene(40, 28)
+    world.device_scene().set_workspace(pool_paths=2000)
     photo = cam.take_photo().samples(9).depth(50).seed(12)
     img = photo.shot(None, world)
     ref, rs = _oracle(world).render(cam.desc, photo.settings(), threads=16)
@@ -322,34 +323,49 @@ def test_per_sample_radiance_vs_oracle(gpu, name):
 
 
 @pytest.mark.parametrize("name", ["rtow", "example_sdl", "quadric_sdl"])
-def test_lanes_and_async_bit_identical(gpu, monkeypatch, name):
-    """Scheduling only: wavefront lanes (concurrent chunk streams, rs_scene_set_lanes), launch grids
-    sized from an earlier frame's path counts (active from the second frame of a workload on) and
-    asynchronous rs_render_device frames all give the first frame bit for bit, which equals the
-    oracle's, with the oracle's world.hit count."""
+def test_streaming_pool_and_async_bit_identical(gpu, name):
+    """Scheduling only. The streaming wavefront (spheres / nest-0 / nest-2 scenes: a pool of paths in
+    flight, camera samples injected per iteration as paths finish) with pools from 20 iterations'
+    worth down to 256 samples per iteration and radiance batches of 1-2 sample planes (several
+    batches in the ring, accumulated while later samples are still traced); chunk lanes; 1-4 frames in
+    flight with asynchronous rs_render_device frames overlapping on one stream -- two frame settings
+    alternating into two buffers, and the row shares r::4 of one frame (a strong-scaled rank's work)
+    into one buffer. Every frame equals the oracle's bit for bit, with the oracle's world.hit count."""
     import torch
-    monkeypatch.setenv("RS_WF_CHUNK", "20000")         # several chunks per batch: every lane busy
     build = {"rtow": lambda: scenes.rtow_13_1(96, 60)[:2], "example_sdl": lambda: scenes.example_sdl(96, 60),
              "quadric_sdl": lambda: scenes.quadric_sdl(96, 60)}[name]
     cam, world = build()
-    photo = cam.take_photo().samples(16).depth(12).seed(5)
     ds = world.device_scene()
-    st = photo.settings()
-    ref, rstats = _oracle(world).render(cam.desc, st)
-    frames = []
-    for lanes in (1, 2, 3, 4, 1, 2):
-        ds.set_lanes(lanes)
-        img, stats = ds.render(cam.desc, st)
-        frames.append(img)
-        assert stats.segments == rstats.segments
-    out = torch.zeros((60, 96, 4), dtype=torch.float32, device="cuda")
+    st = cam.take_photo().samples(16).depth(12).seed(5).settings()
+    st2 = cam.take_photo().samples(9).depth(7).seed(6).settings()
+    orc = _oracle(world)
+    ref, rstats = orc.render(cam.desc, st)
+    ref2, _ = orc.render(cam.desc, st2)
+    npx = 96 * 60
+    for batch, pool in ((32 << 20, 16 << 20), (32 << 20, 20000), (2 * npx, 5000), (npx, 256 * 12)):
+        ds.set_workspace(batch, pool)
+        for lanes in (1, 2):
+            ds.set_lanes(lanes)
+            img, stats = ds.render(cam.desc, st)
+            assert stats.segments == rstats.segments, (batch, pool, lanes)
+            assert np.array_equal(img, ref), (batch, pool, lanes)
+    ds.set_workspace(32 << 20, 16 << 20)
     s = torch.cuda.current_stream().cuda_stream
-    for _ in range(3):  # asynchronous frames back to back on one stream
-        assert ds.render_device(cam.desc, st, out.data_ptr(), s, stats=False) is None
-    torch.cuda.synchronize()
-    frames.append(out.cpu().numpy())
-    for f in frames:
-        assert np.array_equal(f, ref)
+    for frames in (1, 2, 3, 4):
+        ds.set_frames_in_flight(frames)
+        outs = [torch.full((60, 96, 4), -1.0, dtype=torch.float32, device="cuda") for _ in range(2)]
+        for k in range(6):  # two settings alternating, asynchronous, back to back on one stream
+            assert ds.render_device(cam.desc, st if k % 2 == 0 else st2, outs[k % 2].data_ptr(), s, stats=False) is None
+        torch.cuda.synchronize()
+        assert np.array_equal(outs[0].cpu().numpy(), ref), frames
+        assert np.array_equal(outs[1].cpu().numpy(), ref2), frames
+        share = torch.zeros((60, 96, 4), dtype=torch.float32, device="cuda")
+        for r in range(4):  # the row shares of N = 4 ranks, overlapping, into one frame
+            sh = cam.take_photo().samples(16).depth(12).seed(5).rows(r, 0, 4).settings()
+            ds.render_device(cam.desc, sh, share.data_ptr(), s, stats=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(share.cpu().numpy(), ref), frames
+    ds.set_frames_in_flight(2)
 
 
 def test_queue_counter_reset_across_frames(gpu):
