@@ -22,7 +22,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-LANES = int(os.environ.get("RS_LANES", "2"))  # wavefront lanes of the timed region (rs_scene_set_lanes)
+LANES = int(os.environ.get("RS_LANES", "0"))  # wavefront lanes of the timed region (rs_scene_set_lanes; 0 = defaults)
+FRAMES = int(os.environ.get("RS_FRAMES", "0"))  # frames in flight (rs_scene_set_frames_in_flight; 0 = default 2)
 
 
 def log(*a):
@@ -125,6 +126,8 @@ def main():
     photo = cam.take_photo().samples(args.spp).depth(args.depth).seed(args.seed).mode(args.mode)
     ds = scene_world.device_scene()  # BVH build + upload: outside the timed region
     ds.set_lanes(LANES)
+    if FRAMES:
+        ds.set_frames_in_flight(FRAMES)
     H, W = args.height, args.width
     frame = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     last = {}
@@ -163,11 +166,20 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     samples = last["samples"]
+    # the frame latency: frames one at a time, each waited for (the timed region above is the pipelined
+    # throughput of back-to-back asynchronous frames, rs_scene_set_frames_in_flight)
+    lat = []
+    for _ in range(min(args.steps, 5)):
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t2)
+    latency_ms = sorted(lat)[len(lat) // 2] * 1e3
     # the dominant kernel's launches, event-timed (the events ride on the dispatches themselves), and
-    # the library's byte / segment counts: the same K frames again with stats, on ONE wavefront lane
-    # so that no launch shares the GPU with the other lane's kernels (the timed region runs two lanes,
-    # whose overlapping launches would stretch every duration); tools/isolated_kernel_stats.py reads
-    # the same isolated dispatches out of a rocprofv3 trace of this command
+    # the library's byte / segment counts: the same K frames again with stats, synchronous and on ONE
+    # wavefront lane, so that no launch shares the GPU with another lane's or frame's kernels
+    # (concurrent launches would stretch every duration)
     ds.set_lanes(1)
     timed["on"] = True
     kern_ms = 0.0
@@ -230,20 +242,36 @@ def main():
         kname = KERNEL_NAMES.get(last["stats"].kernel_id)
         avg_launch_s = kern_ms / max(1, kern_launches) / 1e3
         bytes_per_launch = kern_bytes / max(1, kern_launches)
-        achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         traffic, traffic_round = load_pmc(kname) if kname else (None, None)
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_profile": traffic_round,
-                "kernel": kname, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                "alg_bytes_per_launch": int(bytes_per_launch), "launches_per_step": kern_launches // args.steps,
-                "kernel_share_of_step": round(kern_ms / args.steps / (dt / args.steps * 1e3), 4),
-                "segments_per_sample": round(segs / max(1, samples), 4), "measured_lanes": 1}
-        # SURVEY 8(d)'s fixed fp32 model for the same kernel: extend reads a 28 B ray and writes a 16 B
-        # hit per segment (44 B); the builder's f64 byte model above is the `frac` field
+        # SURVEY 8(d)'s algorithmic bytes for the dominant kernel (the contract's `achieved`): the extend
+        # reads a 28 B ray and writes a 16 B hit per segment, 44 B per world.hit call
         seg_per_launch = segs / max(1, kern_launches)
+        alg = 44.0 * seg_per_launch
+        achieved = alg / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": kname, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                "alg_bytes_per_launch": int(alg), "alg_model": "SURVEY 8(d): 44 B per segment (28 B ray in, 16 B hit out)",
+                "segments_per_launch": int(seg_per_launch), "launches_per_step": kern_launches // args.steps,
+                "kernel_share_of_step": round(kern_ms / args.steps / (dt / args.steps * 1e3), 4),
+                "segments_per_sample": round(segs / max(1, samples), 4)}
+        # the library's own f64 byte model of the same launches (rs_render_stats.kernel_bytes: the
+        # 32-byte path records, hits, queue slots and radiance this kernel actually moves), secondary
         if avg_launch_s > 0:
-            roof["achieved_s8d"] = round(44.0 * seg_per_launch / avg_launch_s / 1e9, 2)
-            roof["frac_s8d"] = round(roof["achieved_s8d"] / HBM_PEAK_GBS, 5)
+            roof["achieved_lib"] = round(bytes_per_launch / avg_launch_s / 1e9, 2)
+            roof["frac_lib"] = round(roof["achieved_lib"] / HBM_PEAK_GBS, 5)
+            roof["lib_bytes_per_launch"] = int(bytes_per_launch)
+        if traffic is not None:
+            # PMC bytes per launch of this kernel from rocprofv3 --pmc passes of this same command
+            # (tools/gpu.sh pmc -> profiles/pmc_summary.json)
+            roof["traffic_profile"] = traffic_round
+            roof["traffic_derivation"] = ("2 x FETCH_SIZE + WRITE_SIZE per launch: on gfx950 every L2 read request to "
+                                          "the fabric (TCC_EA0_RDREQ) is 128 B and FETCH_SIZE counts 64 B of it, for "
+                                          "coalesced 4-32 B/lane reads and 16 B gathers alike; WRITE_SIZE is exact for "
+                                          "32 B/lane stores (calibrated on known byte counts: tools/micro/pmc_calib.hip, "
+                                          "profiles/r4/calib); counts L2 misses served by the Infinity Cache as well")
+            roof["traffic_over_alg"] = round(traffic / alg, 3) if alg else None
+            roof["traffic_over_lib"] = round(traffic / bytes_per_launch, 3) if bytes_per_launch else None
         cpu = None
         if args.cpu_baseline and world == 1:
             log("timing CPU baseline (oracle restatement) ...")
@@ -253,10 +281,12 @@ def main():
             "metric": "Msamples/s (whole node) + ms/frame, RTIOW-13.1 scene 800x500x64spp",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "frame_latency_ms": round(latency_ms, 4),
             "scaling": "weak" if args.split == "passes" else "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: RTIOW final scene regenerated from seed 7 (restated ChaCha12), per-sample RNG streams",
             "config": {"workload": f"rtow_13_1 balls_scene(seed 7)+light, {W}x{H}, {n_eff} spp, depth {args.depth}",
-                       "width": W, "height": H, "spp": n_eff, "depth": args.depth, "split": args.split, "lanes": LANES,
+                       "width": W, "height": H, "spp": n_eff, "depth": args.depth, "split": args.split,
+                       "lanes": LANES or "default", "frames_in_flight": FRAMES or "default",
                        "samples_per_frame": W * H * n_eff, "frames_per_step": world if args.split == "passes" else 1},
             "roofline": roof,
             "cpu_baseline": cpu,

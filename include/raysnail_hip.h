@@ -273,11 +273,12 @@ int rs_scene_commit(rs_scene* s);
  * works, rendering returns RS_E_STATE. */
 int rs_scene_commit_devices(rs_scene* s, const int* devices, int n);
 int rs_scene_get_info(const rs_scene* s, rs_scene_info* out);
-/* wavefront lanes for the scene's later renders (1 .. 4): concurrent streams within one frame. The
- * bounce-synchronous wavefront (flat / mesh and rich scenes) deals the chunks of a batch to them
- * round robin (default 2); the streaming wavefront (spheres / box / CSG scenes) deals whole sample
- * batches to lanes, each with its own pool of paths (default 1). No reference counterpart (a
- * scheduling knob like Painter::threads, painter.rs:318-325); frames are bitwise the same. */
+/* wavefront lanes for the scene's later renders (1 .. 4; 0 = the defaults): concurrent streams within
+ * one frame. The bounce-synchronous wavefront (flat / mesh and rich scenes) deals the chunks of a
+ * batch to them round robin (default 2); the streaming wavefront (spheres / box / CSG scenes) deals
+ * whole sample batches to lanes, each with its own pool of paths (default 1). No reference
+ * counterpart (a scheduling knob like Painter::threads, painter.rs:318-325); frames are bitwise the
+ * same. */
 int rs_scene_set_lanes(rs_scene* s, uint32_t lanes);
 /* frames in flight per device (1 .. 4; default 2): consecutive asynchronous frames are dealt to this
  * many frame slots, each with its own streams and buffers, and a frame waits only for the previous
@@ -296,6 +297,17 @@ int rs_scene_set_workspace(rs_scene* s, uint64_t max_batch_items, uint64_t pool_
 /* host output: out_rgba = W*H*4 floats; mask = W*H bytes or NULL (all pixels) */
 int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st,
               const uint8_t* mask, float* out_rgba, rs_render_stats* stats);
+/* host output with progressive row delivery -- Painter::draw's PainterTarget::register_pixels
+ * (painter.rs:214) and its end-of-pass sentinel (painter.rs:332). The call's row lattice is rendered
+ * in `bands` bands (0 = 16) of consecutive lattice rows, several in flight at once
+ * (rs_scene_set_frames_in_flight per device, bands dealt to the devices round robin); as soon as a
+ * band is complete, cb(user, y, row, W) is called for each of its rows y (row = out_rgba's row y,
+ * already written), from the calling thread, in band order, while the later bands are traced; then
+ * cb(user, H, NULL, 0). Rows off the lattice are neither written nor reported. The frame is bitwise
+ * the rs_render frame. With stats, bands are rendered one at a time (timed). */
+typedef void (*rs_row_callback)(void* user, uint32_t y, const float* row_rgba, uint32_t width);
+int rs_render_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask,
+                   float* out_rgba, uint32_t bands, rs_row_callback cb, void* user, rs_render_stats* stats);
 /* device output: d_out_rgba device pointer (W*H*4 floats), d_mask device pointer or NULL,
  * stream = hipStream_t or NULL (default stream). With stats != NULL the call returns after the
  * work is enqueued AND complete (it synchronises its stream) so that stats are final, and times

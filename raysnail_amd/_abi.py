@@ -135,6 +135,9 @@ SCENE_SIGNATURES = {
     "constant_medium": (C.c_int, [VP, C.c_uint32, C.POINTER(C.c_float), C.c_double, U32P]),
 }
 
+# rs_row_callback: (user, y, row_rgba, width)
+ROW_CALLBACK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.POINTER(C.c_float), C.c_uint32)
+
 _LIB = None
 ABI_VERSION = 5  # include/raysnail_hip.h RS_ABI_VERSION
 
@@ -186,6 +189,9 @@ def load() -> C.CDLL:
     lib.rs_scene_commit_devices.argtypes = [VP, C.POINTER(C.c_int), C.c_int]
     lib.rs_scene_set_lanes.argtypes = [VP, C.c_uint32]
     lib.rs_scene_set_frames_in_flight.argtypes = [VP, C.c_uint32]
+    lib.rs_render_rows.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), VP, VP, C.c_uint32,
+                                   ROW_CALLBACK, VP, C.POINTER(rs_render_stats)]
+    lib.rs_render_rows.restype = C.c_int
     lib.rs_scene_set_workspace.argtypes = [VP, C.c_uint64, C.c_uint64]
     for fn in ("rs_probe_world_hit", "rs_scene_get_info", "rs_scene_set_lanes", "rs_scene_set_frames_in_flight",
                "rs_scene_set_workspace", "rs_scene_commit_devices", "rs_scene_create", "rs_scene_destroy",
@@ -203,6 +209,6 @@ EXPORTED_SYMBOLS = [
     "rs_scene_destroy", "rs_perlin", "rs_image", "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
     "rs_difference", "rs_transformed", "rs_constant_medium", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
     "rs_scene_commit", "rs_scene_commit_devices", "rs_scene_get_info", "rs_scene_set_lanes",
-    "rs_scene_set_frames_in_flight", "rs_scene_set_workspace", "rs_render", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
+    "rs_scene_set_frames_in_flight", "rs_scene_set_workspace", "rs_render", "rs_render_rows", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
     "rs_probe_world_hit", "rs_probe_samples",
 ]

@@ -575,6 +575,34 @@ class DeviceScene:
                                             out.ctypes.data_as(C.c_void_p), C.byref(stats)), "rs_")
         return out, stats
 
+    def render_rows(self, cam: A.rs_camera_desc, st: A.rs_render_settings, on_row, mask: Optional[np.ndarray] = None,
+                    bands: int = 16, stats: bool = True) -> Tuple[np.ndarray, Optional[A.rs_render_stats]]:
+        """rs_render_rows: on_row(y, out) is called for each lattice row y as soon as its band is complete
+        (out[y] holds it), in lattice order, from this thread; then on_row(H, out) (the sentinel)."""
+        H, W = cam.height, cam.width
+        out = np.zeros((H, W, 4), dtype=np.float32)
+        mptr = None
+        if mask is not None:
+            mask = np.ascontiguousarray(mask, dtype=np.uint8).reshape(H * W)
+            mptr = mask.ctypes.data_as(C.c_void_p)
+        err = []
+
+        def cb(user, y, row, width):
+            if err:
+                return
+            try:  # no exception may cross the C ABI: kept and raised after the call
+                on_row(int(y), out)
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+        ccb = A.ROW_CALLBACK(cb)
+        st_out = A.rs_render_stats() if stats else None
+        _check(self.lib, self.lib.rs_render_rows(self.handle, C.byref(cam), C.byref(st), mptr,
+                                                 out.ctypes.data_as(C.c_void_p), bands, ccb, None,
+                                                 C.byref(st_out) if stats else None), "rs_")
+        if err:
+            raise err[0]
+        return out, st_out
+
     def render_device(self, cam: A.rs_camera_desc, st: A.rs_render_settings, d_out_ptr: int,
                       stream_ptr: int = 0, d_mask_ptr: int = 0, stats: bool = True):
         """rs_render_device. stats=True: synchronous, returns rs_render_stats (kernel timing included);
@@ -729,34 +757,22 @@ class TakePhotoSettings:
             out, stats = world.device_scene().render(cam, st, mask)
             self.last_stats = stats
             return out
-        # progressive delivery (painter.rs:214 registers each row as a worker finishes it): the row
-        # lattice in 8 bands, each band's rows handed over when the band is done; pixels do not depend
-        # on the banding (per-sample RNG streams), so the frame equals the one-call frame
+        # progressive delivery (painter.rs:214 registers each row as a worker finishes it):
+        # rs_render_rows hands each band of the row lattice over as soon as it is complete, later bands
+        # still in flight; pixels do not depend on the banding (per-sample RNG streams), so the frame
+        # equals the one-call frame. Rows off the lattice (all zero) are registered before the sentinel.
         H = cam.height
-        rb, step = st.row_begin, st.row_step or 1
-        re = min(st.row_end, H) if st.row_end else H
-        rows = list(range(rb, re, step))
-        per = max(1, -(-len(rows) // 8))
-        out = np.zeros((H, cam.width, 4), np.float32)
-        total = A.rs_render_stats()
-        sent = set()
-        for k in range(0, len(rows), per):
-            band = rows[k:k + per]
-            bs = self.settings()
-            bs.row_begin, bs.row_end, bs.row_step = band[0], band[-1] + 1, step
-            img, s = world.device_scene().render(cam, bs, mask)
-            for f in ("samples", "segments", "ms", "path_ms", "launches", "kernel_launches", "kernel_ms", "kernel_bytes"):
-                setattr(total, f, getattr(total, f) + getattr(s, f))
-            total.kernel_id, total.tree_arity = s.kernel_id, s.tree_arity
-            for y in band:
-                out[y] = img[y]
-                target.register_pixels(y, out[y])
-                sent.add(y)
-        for y in range(H):  # rows off the lattice (all zero), once each
-            if y not in sent:
-                target.register_pixels(y, out[y])
-        self.last_stats = total
-        target.register_pixels(H, [])  # end-of-pass sentinel (painter.rs:332)
+        sent = np.zeros(H, dtype=bool)
+
+        def on_row(y, out):
+            if y == H:
+                for r in np.flatnonzero(~sent):
+                    target.register_pixels(int(r), out[r])
+                target.register_pixels(H, [])  # end-of-pass sentinel (painter.rs:332)
+                return
+            sent[y] = True
+            target.register_pixels(y, out[y])
+        out, self.last_stats = world.device_scene().render_rows(cam, st, on_row, mask)
         return out
 
     def shot(self, path, world: World) -> np.ndarray:

@@ -1078,7 +1078,18 @@ void build(rs_scene* s) {
             if (s->objs[h].kind == PK_SPHERE) lsph[h] = spheres[prims[h].idx];
         // the kernels address this array with 32-bit byte offsets (rs_kernels.hip ld_sphere)
         if (lsph.size() * sizeof(DSphere) > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "scene too large: sphere array over 4 GiB");
-        stage(s, d.lsph, lsph);
+        if (d.moving) {
+            stage(s, d.lsph, lsph);
+        } else {  // 32-byte records (DSphereS): the static spheres' leaf data in half the cache lines
+            std::vector<DSphereS> lsphs(lsph.size());
+            for (size_t h = 0; h < lsph.size(); ++h) {
+                for (int k = 0; k < 3; ++k) lsphs[h].c[k] = lsph[h].c[k];
+                lsphs[h].r = lsph[h].r;
+                if (s->objs[h].kind == PK_SPHERE && lsph[h].r * lsph[h].r != lsph[h].r2)
+                    throw Error(RS_E_INVALID, "sphere radius_squared is not radius * radius");
+            }
+            stage(s, d.lsphs, lsphs);
+        }
     }
     if (s->scene_mode == kSmFlat) {
         std::vector<LTri> ltri(leaves.prims.size());
@@ -1981,6 +1992,93 @@ void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
     if (stats) *stats = acc;
 }
 
+// rs_render_rows: the frame's row lattice in bands, each band a frame of its own on the replicas'
+// frame slots (band b on replica b % n), up to frames_in_flight bands in flight per replica; each
+// band's rows are copied to pinned host memory on the replica's stream, and once a band's copy is
+// complete its rows are handed to the callback -- from the calling thread, in band order, while the
+// later bands are traced (painter.rs:214's register_pixels as rows finish), then the sentinel.
+void render_frame_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask,
+                       float* out, uint32_t bands, rs_row_callback cb, void* user, rs_render_stats* stats) {
+    if (!out || !cb) throw Error(RS_E_INVALID, "null argument");
+    validate_render(s, cam, st);
+    rs_render_stats acc{};
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t n = (uint32_t)s->reps.size();
+    const uint32_t W = cam->width, H = cam->height;
+    const size_t npx = (size_t)W * H;
+    const uint32_t rb = st->row_begin, re = st->row_end ? std::min(st->row_end, H) : H;
+    const uint32_t step = st->row_step ? st->row_step : 1;
+    const uint32_t n_rows = rb < re ? (re - rb + step - 1) / step : 0;
+    if (bands == 0) bands = 16;
+    const uint32_t per = std::max<uint32_t>(1, (n_rows + bands - 1) / bands);
+    const uint32_t n_bands = n_rows ? (n_rows + per - 1) / per : 0;
+    const uint32_t ahead = std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+    float* pinned = nullptr;
+    std::vector<std::unique_ptr<Pending>> P(n_bands);
+    std::vector<hipEvent_t> copied(n_bands, nullptr);
+    std::vector<RowSet> rows(n_bands);
+    std::vector<uint8_t*> d_masks(n, nullptr);
+    auto cleanup = [&]() {
+        for (uint32_t k = 0; k < n; ++k) {
+            DeviceGuard g(s->reps[k]->device);
+            (void)hipStreamSynchronize(s->reps[k]->stream);
+            if (d_masks[k]) (void)hipFree(d_masks[k]);
+        }
+        for (hipEvent_t e : copied) if (e) (void)hipEventDestroy(e);
+        if (pinned) (void)hipHostFree(pinned);
+    };
+    try {
+        HIP_OK(hipHostMalloc((void**)&pinned, npx * 4 * sizeof(float)));
+        std::memcpy(pinned, out, npx * 4 * sizeof(float));  // rows off the lattice keep the caller's values
+        if (mask)
+            for (uint32_t k = 0; k < n; ++k) {  // the mask once per replica, read by all its bands
+                DeviceGuard g(s->reps[k]->device);
+                HIP_OK(hipMalloc((void**)&d_masks[k], npx));
+                HIP_OK(hipMemcpyAsync(d_masks[k], mask, npx, hipMemcpyHostToDevice, s->reps[k]->stream));
+            }
+        auto enqueue = [&](uint32_t b) {
+            Replica& R = *s->reps[b % n];
+            DeviceGuard g(R.device);
+            rs_render_settings bs = *st;
+            bs.row_begin = rb + b * per * step;
+            bs.row_end = (uint32_t)std::min<uint64_t>(re, (uint64_t)bs.row_begin + (uint64_t)per * step);
+            bs.row_step = step;
+            rows[b] = replica_rows(cam, &bs, 0, 1);
+            const uint32_t n_slots = s->stack_need > kStackMax ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            Slot& L = R.slots[R.next_slot % n_slots];
+            if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
+            ensure(L, L.d_out, L.out_cap, npx * 4);
+            P[b].reset(new Pending());
+            render_enqueue(s, R, cam, &bs, rows[b], d_masks[b % n], L.d_out, R.stream, *P[b], stats != nullptr);
+            HIP_OK(copy_rows(pinned, L.d_out, W, rows[b], hipMemcpyDeviceToHost, R.stream));
+            HIP_OK(hipEventRecord(L.free_ev, R.stream));  // the copy read the slot's frame
+            HIP_OK(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
+            HIP_OK(hipEventRecord(copied[b], R.stream));
+        };
+        for (uint32_t b = 0; b < std::min(n_bands, ahead * n); ++b) enqueue(b);
+        for (uint32_t b = 0; b < n_bands; ++b) {
+            {
+                DeviceGuard g(s->reps[b % n]->device);
+                if (stats) render_finish(s, *P[b], &acc);  // (statistics: the band's share, synchronous)
+                HIP_OK(hipEventSynchronize(copied[b]));
+            }
+            if (b + ahead * n < n_bands) enqueue(b + ahead * n);
+            for (uint32_t y = rows[b].begin; y < rows[b].end; y += rows[b].step) {
+                std::memcpy(out + (size_t)y * W * 4, pinned + (size_t)y * W * 4, (size_t)W * 4 * sizeof(float));
+                cb(user, y, out + (size_t)y * W * 4, W);
+            }
+        }
+    } catch (...) {
+        cleanup();
+        throw;
+    }
+    cleanup();
+    cb(user, H, nullptr, 0);  // end-of-pass sentinel (painter.rs:332)
+    acc.tree_arity = s->tree_arity;
+    acc.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = acc;
+}
+
 }  // namespace
 
 namespace {
@@ -2241,9 +2339,9 @@ int rs_scene_commit_devices(rs_scene* s, const int* devices, int n) {
 int rs_scene_set_lanes(rs_scene* s, uint32_t lanes) {
     return run([&] {
         if (!s) throw Error(RS_E_INVALID, "null argument");
-        if (lanes < 1 || lanes > kMaxLanes) throw Error(RS_E_INVALID, "lanes must be 1 .. 4");
-        s->wf_lanes = lanes;
-        s->stream_lanes = lanes;
+        if (lanes > kMaxLanes) throw Error(RS_E_INVALID, "lanes must be 0 (defaults) or 1 .. 4");
+        s->wf_lanes = lanes ? lanes : 2;
+        s->stream_lanes = lanes ? lanes : 1;
     });
 }
 int rs_scene_set_frames_in_flight(rs_scene* s, uint32_t frames) {
@@ -2391,6 +2489,13 @@ int rs_probe_samples(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
         HIP_OK(launch_probe_sample(R.ref(), make_camera(*cam), pp, s->scene_mode, x, y, s0, n, dout, nullptr));
         HIP_OK(hipMemcpy(out, dout, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(dout);
+    });
+}
+
+int rs_render_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask,
+                   float* out_rgba, uint32_t bands, rs_row_callback cb, void* user, rs_render_stats* stats) {
+    return run([&] {
+        render_frame_rows(S(s), cam, st, mask, out_rgba, bands, cb, user, stats);
     });
 }
 

@@ -226,6 +226,17 @@ __device__ __forceinline__ DSphere ld_sphere(const DScene& S, const DSphere* arr
     return s;
 }
 
+// A static sphere from its 32-byte record: r2 = r * r is radius_squared's own f64 product (sphere.rs:40)
+__device__ __forceinline__ DSphere ld_sphere_s(const DSphereS* arr, int i) {
+    const uint32_t o = (uint32_t)i * (uint32_t)sizeof(DSphereS);
+    const d2v a = gld<d2v>(arr, o), b = gld<d2v>(arr, o + 16);
+    DSphere s;
+    s.c[0] = a.x; s.c[1] = a.y; s.c[2] = b.x; s.r = b.y;
+    s.r2 = s.r * s.r;
+    s.v[0] = s.v[1] = s.v[2] = 0.0;
+    return s;
+}
+
 // A leaf-ordered triangle record (80 B) through five 16-byte global loads
 __device__ __forceinline__ LTri ld_ltri(const LTri* arr, int i) {
     const uint32_t o = (uint32_t)i * (uint32_t)sizeof(LTri);
@@ -288,7 +299,7 @@ template <int SM>
 __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, const RayC& rc, double tmin, double& best,
                                           double& bend, int& bp) {
     if (SM == kSmSpheres) {  // prim-indexed sphere copy: no DPrim hop (e is the prim in this mode)
-        test_sphere_leaf(S, ld_sphere(S, S.lsph, e), e, r, rc, tmin, best, bend, bp);
+        test_sphere_leaf(S, S.moving ? ld_sphere(S, S.lsph, e) : ld_sphere_s(S.lsphs, e), e, r, rc, tmin, best, bend, bp);
         return;
     }
     if (SM == kSmFlat) {  // leaf-ordered triangle copy; its `kind` field says whether entry e is one
@@ -1280,13 +1291,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const 
                 const uint32_t perm = gen_perm(jb, 0, nb, P);
                 item += perm;
                 live = camera_sample(C, P, g0 + perm, r, rng);
-                if (!live) {
-                    rad[item] = 0.0; rad[I.ring + item] = 0.0; rad[2 * I.ring + item] = 0.0;
-                } else {
-                    // the record is written before the traversal (most camera samples go on to
-                    // shading), so the RNG state is not held in registers across it
-                    store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
-                }
+                if (!live) { rad[item] = 0.0; rad[I.ring + item] = 0.0; rad[2 * I.ring + item] = 0.0; }
             } else {
                 r = load_ray(cur, i);
                 live = true;
@@ -1325,13 +1330,19 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const 
                         cls = -1;
                     } else {
                         W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+                        // a camera sample that goes on to shading: its record (T = 1, level 0); a carried
+                        // path's is in place
+                        if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
                         done = false;
                     }
                 }
                 if (done) {  // 0 + T * add: the path's radiance so far is 0 (WfSet)
-                    // (a camera sample's record was written by this thread before the traversal: T = 1)
-                    const D4 t4 = cur.thr[i];
-                    item = cur.tag[i].x;
+                    D4 t4;
+                    if (gen) {
+                        t4.x = t4.y = t4.z = 1.0;
+                    } else {
+                        t4 = cur.thr[i]; item = cur.tag[i].x;
+                    }
                     rad[item] = 0.0 + t4.x * add.x;
                     rad[I.ring + item] = 0.0 + t4.y * add.y;
                     rad[2 * I.ring + item] = 0.0 + t4.z * add.z;

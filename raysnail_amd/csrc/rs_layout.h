@@ -37,6 +37,13 @@ struct DSphere {   // sphere.rs:16-23
     double v[3];   // speed
 };
 
+// A static sphere in 32 bytes (spheres-only scenes without motion: the traversal's leaf record):
+// radius_squared is radius * radius (sphere.rs:35-43), recomputed by the same f64 multiply.
+struct alignas(32) DSphereS {
+    double c[3];
+    double r;
+};
+
 struct DRect {     // rect.rs:178-212
     int32_t ax0, ax1, ax2, pad;
     double k, a0, a1, b0, b1;
@@ -157,6 +164,7 @@ struct DScene {
     const DSphere* spheres;
     const int32_t* lprim;    // leaf entry -> prim handle (flat scenes; null: leaf codes are ~prim)
     const DSphere* lsph;     // spheres-only scenes: the sphere of prim handle p at lsph[p] (no DPrim hop)
+    const DSphereS* lsphs;   // the same in 32-byte records when no sphere moves (twice the records per cache line)
     const LTri* ltri;        // flat scenes: the triangle of each leaf entry (+ every entry's kind)
     const DRect* rects;
     const DBox* boxes;

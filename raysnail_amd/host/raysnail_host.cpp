@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
 
 #include "raysnail.hpp"
@@ -367,34 +368,39 @@ std::vector<Pixel> TakePhotoSettings::shot_to_target(const char*, World& world, 
         return out;
     }
     // Progressive delivery: upstream's workers call register_pixels as each row finishes
-    // (painter.rs:214), which feeds the CLI preview. Here the frame's row lattice is rendered in
-    // kBands bands and each band's rows are handed over as soon as the band is done. Pixels do not
-    // depend on the banding (every sample has its own RNG stream), so the frame is the one-call frame.
-    constexpr uint32_t kBands = 8;
-    const uint32_t rb = st.row_begin, re = st.row_end ? std::min<uint32_t>(st.row_end, (uint32_t)H) : (uint32_t)H;
-    const uint32_t step = st.row_step ? st.row_step : 1;
-    const uint32_t n_rows = rb < re ? (re - rb + step - 1) / step : 0;
-    const uint32_t per = std::max<uint32_t>(1, (n_rows + kBands - 1) / kBands);
-    std::vector<uint8_t> sent(H, 0);
-    stats_ = rs_render_stats{};
-    for (uint32_t r0 = 0; r0 < n_rows; r0 += per) {
-        rs_render_settings bs = st;
-        bs.row_begin = rb + r0 * step;
-        bs.row_end = (uint32_t)std::min<uint64_t>(re, (uint64_t)bs.row_begin + (uint64_t)per * step);
-        bs.row_step = step;
-        rs_render_stats s{};
-        check_rs(rs_render(world.device_scene(), &cam, &bs, mp, reinterpret_cast<float*>(out.data()), &s));
-        stats_.samples += s.samples; stats_.segments += s.segments; stats_.ms += s.ms; stats_.path_ms += s.path_ms;
-        stats_.launches += s.launches; stats_.kernel_launches += s.kernel_launches; stats_.kernel_ms += s.kernel_ms;
-        stats_.kernel_bytes += s.kernel_bytes; stats_.kernel_id = s.kernel_id; stats_.tree_arity = s.tree_arity;
-        for (uint32_t y = bs.row_begin; y < bs.row_end; y += step) {
-            target->register_pixels(y, std::vector<Pixel>(out.begin() + (size_t)y * W, out.begin() + ((size_t)y + 1) * W));
-            sent[y] = 1;
+    // (painter.rs:214), which feeds the CLI preview. rs_render_rows renders the frame's row lattice in
+    // bands, several in flight, and hands each band's rows over as soon as the band is complete, while
+    // the later bands are traced; pixels do not depend on the banding (every sample has its own RNG
+    // stream), so the frame is the one-call frame. Rows off the lattice (untouched, all zero) are
+    // registered before the end-of-pass sentinel (painter.rs:332).
+    struct Ctx {
+        PainterTarget* target;
+        size_t W, H;
+        std::vector<uint8_t> sent;
+        const std::vector<Pixel>* out;
+        std::exception_ptr err;
+    } ctx{target, W, H, std::vector<uint8_t>(H, 0), &out, nullptr};
+    rs_row_callback cb = [](void* u, uint32_t y, const float* row, uint32_t w) {
+        Ctx& c = *static_cast<Ctx*>(u);
+        if (c.err) return;
+        try {  // (no exception may cross the C ABI: kept and rethrown after the call)
+            if (y == c.H) {
+                for (size_t r = 0; r < c.H; ++r)
+                    if (!c.sent[r]) c.target->register_pixels(r, std::vector<Pixel>(c.out->begin() + r * c.W, c.out->begin() + (r + 1) * c.W));
+                c.target->register_pixels(c.H, {});
+                return;
+            }
+            c.sent[y] = 1;
+            std::vector<Pixel> px(w);
+            std::memcpy(px.data(), row, (size_t)w * sizeof(Pixel));
+            c.target->register_pixels(y, px);
+        } catch (...) {
+            c.err = std::current_exception();
         }
-    }
-    for (size_t y = 0; y < H; ++y)  // rows off the lattice (untouched: all zero), once each
-        if (!sent[y]) target->register_pixels(y, std::vector<Pixel>(out.begin() + y * W, out.begin() + (y + 1) * W));
-    target->register_pixels(H, {});  // end-of-pass sentinel (painter.rs:332)
+    };
+    stats_ = rs_render_stats{};
+    check_rs(rs_render_rows(world.device_scene(), &cam, &st, mp, reinterpret_cast<float*>(out.data()), 16, cb, &ctx, &stats_));
+    if (ctx.err) std::rethrow_exception(ctx.err);
     return out;
 }
 

@@ -7,6 +7,7 @@
 #include <dlfcn.h>
 
 #include <cmath>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -157,6 +158,34 @@ int main(int argc, char** argv) {
               (unsigned long long)photo.last_stats().segments, (unsigned long long)ost.segments);
         std::printf("mode %d: %zu/%zu pixels equal, segments %llu\n", mode, same, W * H,
                     (unsigned long long)ost.segments);
+    }
+
+    // progressive delivery (painter.rs:214): rows arrive, in lattice order, while later bands of the
+    // frame are still being traced; then the sentinel; the frame equals the one-call frame
+    {
+        Camera big = CameraBuilder().look_from({8, 3, 6}).look_at({0, 0.6, 0}).fov(35).aperture(0.05)
+                         .focus_to_look_at().shutter_speed(1.0).width(480).height(270).build();
+        TakePhotoSettings photo = big.take_photo();
+        photo.samples(64).depth(12).seed(3);
+        struct Timed : PainterTarget {
+            std::chrono::steady_clock::time_point t0;
+            std::vector<size_t> ys;
+            std::vector<double> ms;
+            void register_pixels(size_t y, const std::vector<Pixel>&) override {
+                ys.push_back(y);
+                ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+            }
+        } tr;
+        tr.t0 = std::chrono::steady_clock::now();
+        std::vector<Pixel> g = photo.shot_to_target(nullptr, world, &tr, nullptr, nullptr);
+        CHECK(tr.ys.size() == 271 && tr.ys.back() == 270, "progressive rows + sentinel");
+        bool ordered = true;
+        for (size_t y = 0; y < 270; ++y) ordered = ordered && tr.ys[y] == y;
+        CHECK(ordered, "rows delivered in lattice order");
+        CHECK(tr.ms[0] < 0.6 * tr.ms.back(), "first row at %.1f ms of a %.1f ms frame", tr.ms[0], tr.ms.back());
+        std::vector<Pixel> one = photo.shot(nullptr, world);
+        CHECK(std::memcmp(g.data(), one.data(), g.size() * sizeof(Pixel)) == 0, "banded frame == one-call frame");
+        std::printf("progressive: first row at %.1f ms, sentinel at %.1f ms\n", tr.ms[0], tr.ms.back());
     }
 
     // progressive passes folded like the CLI (raysnail.rs:379-427)

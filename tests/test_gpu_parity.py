@@ -441,3 +441,30 @@ def test_emissive_and_lambertian_csg_classes(gpu):
     assert photo.last_stats.segments == rs.segments
     assert np.array_equal(img, ref)
     assert img[..., :3].max() > 1.0  # the lamp is seen directly
+
+
+@pytest.mark.parametrize("frames", [1, 2, 3])
+def test_render_rows_progressive(gpu, frames):
+    """rs_render_rows (Painter::draw + PainterTarget::register_pixels, painter.rs:214, 332): every lattice
+    row once, in lattice order, its pixels final when reported, then the (H) sentinel; the frame equals
+    the one-call frame bitwise -- with 1-3 bands in flight, a strided lattice and a pixel mask."""
+    cam, world = scenes.example_sdl(160, 100)
+    ds = world.device_scene()
+    ds.set_frames_in_flight(frames)
+    photo = cam.take_photo().samples(9).depth(8).seed(2)
+    ref, _ = ds.render(cam.desc, photo.settings())
+    for lattice, mask in (((0, 0, 1), None), ((1, 0, 3), (np.arange(160 * 100).reshape(100, 160) % 7 != 0))):
+        st = photo.rows(*lattice).settings()
+        one, _ = ds.render(cam.desc, st, mask)
+        seen = []
+
+        def on_row(y, out):
+            seen.append(y)
+            if y < 100:
+                assert np.array_equal(out[y], one[y]), y
+        for stats in (False, True):
+            seen.clear()
+            img, _ = ds.render_rows(cam.desc, st, on_row, mask, bands=7, stats=stats)
+            assert seen == list(range(lattice[0], 100, lattice[2])) + [100]
+            assert np.array_equal(img[lattice[0]::lattice[2]], one[lattice[0]::lattice[2]])
+    ds.set_frames_in_flight(2)

@@ -1,0 +1,59 @@
+#!/bin/bash
+# GPU-box sessions (one parameterised script; outputs under gpurun_out/<tag>/, copy what is judged into
+# profiles/). Every GPU step has its own time limit and the session stops at the first failure.
+# usage: bash tools/gpu.sh <tag> <step> [<step> ...]
+#   tests    pytest -m gpu (every GPU test)
+#   bench    python bench.py (the driver's line: CPU baseline, row share)
+#   trace    rocprofv3 kernel traces: bench frames (tools/render_once.py) and N=8 row-share frames
+#            (tools/share_frames.py) -> kernel_stats / kernel_trace csv
+#   pmc      FETCH_SIZE / WRITE_SIZE passes over bench frames + profiles/pmc_summary.json (tools/collect_pmc.py)
+#   calib    FETCH_SIZE / WRITE_SIZE / TCC_EA0_RDREQ passes over tools/micro/pmc_calib (known byte counts)
+#   mix      instruction-mix / lane-utilisation PMC passes (tools/pmc_mix.sh) + VALU roofline (tools/valu_roofline.py)
+#            on the bench frame, C4's and C5's scenes
+#   scenes   kernel traces of the C4 / C5 scenes (tools/time_scene.py)
+#   configs  tools/bench_configs.py (C2-C5, X1, X2 vs the CPU oracle on row subsets)
+set -u
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=$1; shift
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() { local t=$1; shift; echo "== $* (limit ${t}s)" >> $OUT/steps.log; timeout -k 10 $t "$@"; local rc=$?; echo "   rc=$rc" >> $OUT/steps.log; return $rc; }
+for s in "$@"; do
+  case $s in
+  tests)
+    (cd $R && step 900 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu > $OUT/pytest_gpu.log 2>&1) || { echo "gpu tests failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+    tail -1 $OUT/pytest_gpu.log ;;
+  bench)
+    (cd $R && step 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err) || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
+    tail -1 $OUT/bench.json ;;
+  trace)
+    (cd /tmp && step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/tools/render_once.py 0 5 > $OUT/trace_frames.log 2>&1) || { echo "trace failed"; exit 1; }
+    (cd /tmp && step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/share -o share -- python3 $R/tools/share_frames.py 8 10 > $OUT/share_frames.log 2>&1) || { echo "share trace failed"; exit 1; } ;;
+  pmc)
+    (cd /tmp && step 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-baseline 0 --row-share 0 > /dev/null 2> $OUT/pmc_fetch.err) || { echo "pmc fetch failed"; exit 1; }
+    (cd /tmp && step 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-baseline 0 --row-share 0 > /dev/null 2> $OUT/pmc_write.err) || { echo "pmc write failed"; exit 1; }
+    FC=$(find $OUT/pmc_fetch -name '*counter_collection.csv' | head -1); WC=$(find $OUT/pmc_write -name '*counter_collection.csv' | head -1)
+    (cd $R && python3 tools/collect_pmc.py "$FC" "$WC" $R/profiles/pmc_summary.json $TAG > /dev/null && cp $R/profiles/pmc_summary.json $OUT/pmc_summary_wavefront.json) || { echo "pmc summary failed"; exit 1; } ;;
+  calib)
+    for c in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+      d=$(echo $c | cut -d' ' -f1)
+      (cd /tmp && step 60 rocprofv3 --pmc $c --output-format csv -d $OUT/calib_$d -o c -- $R/tools/micro/pmc_calib > $OUT/calib_$d.log 2>&1) || { echo "calib $c failed"; tail -5 $OUT/calib_$d.log; exit 1; }
+    done ;;
+  mix)
+    for sc in "rtow 64 8" "quadric_sdl 16 50" "mesh_scene 16 50"; do
+      set -- $sc
+      (cd $R && bash tools/pmc_mix.sh $OUT/mix_$1 - $1 $2 $3 > $OUT/mix_$1.log 2>&1) || { echo "pmc mix $1 failed"; tail -5 $OUT/mix_$1.log; exit 1; }
+      (cd /tmp && step 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/mixtr_$1 -o tr -- python3 $R/tools/render_once.py 0 2 $1 $2 $3 > $OUT/mixtr_$1.log 2>&1) || { echo "mix trace $1 failed"; exit 1; }
+      (cd $R && python3 tools/valu_roofline.py $OUT/mix_$1 $(ls $OUT/mixtr_$1/*kernel_trace.csv) $OUT/valu_$1.json > $OUT/valu_$1.txt 2>&1)
+    done ;;
+  scenes)
+    (cd /tmp && step 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tr_c4 -o tr -- python3 $R/tools/time_scene.py default quadric 16 50 1024x1024 > $OUT/tr_c4.log 2>&1) || { echo "c4 trace failed"; tail -5 $OUT/tr_c4.log; exit 1; }
+    (cd /tmp && step 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tr_c5 -o tr -- python3 $R/tools/time_scene.py default mesh 16 50 1920x1080 > $OUT/tr_c5.log 2>&1) || { echo "c5 trace failed"; tail -5 $OUT/tr_c5.log; exit 1; } ;;
+  configs)
+    (cd $R && step 900 python3 tools/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err) || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
+    cat $OUT/configs.jsonl ;;
+  *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done
