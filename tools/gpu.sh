@@ -8,6 +8,7 @@
 #            (tools/share_frames.py) -> kernel_stats / kernel_trace csv
 #   pmc      FETCH_SIZE / WRITE_SIZE passes over bench frames + profiles/pmc_summary.json (tools/collect_pmc.py)
 #   calib    FETCH_SIZE / WRITE_SIZE / TCC_EA0_RDREQ passes over tools/micro/pmc_calib (known byte counts)
+#   l1       L1 / L2 hit counters over bench frames (TCP / TCC)
 #   mix      instruction-mix / lane-utilisation PMC passes (tools/pmc_mix.sh) + VALU roofline (tools/valu_roofline.py)
 #            on the bench frame, C4's and C5's scenes
 #   scenes   kernel traces of the C4 / C5 scenes (tools/time_scene.py)
@@ -40,6 +41,10 @@ for s in "$@"; do
       d=$(echo $c | cut -d' ' -f1)
       (cd /tmp && step 60 rocprofv3 --pmc $c --output-format csv -d $OUT/calib_$d -o c -- $R/tools/micro/pmc_calib > $OUT/calib_$d.log 2>&1) || { echo "calib $c failed"; tail -5 $OUT/calib_$d.log; exit 1; }
     done ;;
+  l1)
+    # L1 (TCP) tag accesses and misses to L2 with their latency, L2 hits / misses: the traversal's data
+    # locality on the bench frame (one pass: 4 TCP + 2 TCC counters)
+    (cd /tmp && step 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/l1 -o l1 -- python3 $R/tools/render_once.py 0 2 > $OUT/l1.log 2>&1) || { echo "l1 pass failed"; tail -5 $OUT/l1.log; exit 1; } ;;
   mix)
     for sc in "rtow 64 8" "quadric_sdl 16 50" "mesh_scene 16 50"; do
       set -- $sc
