@@ -1833,11 +1833,11 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         for (size_t l = 0; l < P.lanes.size(); ++l)
             for (uint64_t t = 0; t < P.lanes[l].T; ++t) {
                 const uint32_t* q = &P.qc[P.lanes[l].cnt_off + t * kWfsStride];
-                uint64_t live = 0, shaded = 0;
-                for (uint32_t k = 0; k < kStatLines; ++k) live += q[cix(kCntStat0 + (int)k)];
+                uint64_t live_new = 0, shaded = 0;
+                for (uint32_t k = 0; k < kStatLines; ++k) live_new += q[cix(kCntStat0 + (int)k)];
                 for (int k = 0; k < kWfsClasses; ++k) shaded += q[cix(1 + k)];
-                const uint64_t old = q[cix(0)];
-                const uint64_t live_new = live - old, dead_new = P.inj[l][t] - live_new;
+                const uint64_t old = q[cix(0)], live = old + live_new;
+                const uint64_t dead_new = P.inj[l][t] - live_new;
                 const uint64_t ended = live - shaded;
                 seg += live;
                 kbytes += 64ull * old + 20ull * shaded + 104ull * live_new + 60ull * ended + 24ull * dead_new;

@@ -117,8 +117,8 @@ constexpr int kWfsClasses = 5;   // Lambertian, Metal, DiffuseMetal, Dielectric,
 constexpr uint32_t kCntPad = RS_CNT_PAD;
 // counter slots per streaming iteration: 0 paths carried in from the previous iteration, 1-5 class
 // queues, 6 / 7 front / back runs of the next set, 8 .. 8 + kStatLines - 1 the iteration's live
-// segments spread over lines by block (a single word takes only ~88 returning atomics/us; summed by
-// the host)
+// camera samples spread over lines by block (a single word takes only ~88 atomics/us; summed by the
+// host; the iteration's segments are slot 0 + these)
 constexpr int kCntStat0 = 8;
 constexpr uint32_t kStatLines = 8;
 constexpr uint32_t kWfsStride = (kCntStat0 + kStatLines) * kCntPad;

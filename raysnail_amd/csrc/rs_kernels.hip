@@ -1353,11 +1353,13 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const 
 #ifdef RS_TRAV_STATS
         trav_stats_flush(live);
 #endif
-        // the iteration's live segments are counted in the same block reduction, on one of kStatLines
-        // counters by block (one returning-free atomic per block on a single word capped an empty
-        // camera-ray launch at ~88 atomics/us: 1.14 ms for 25.6 M samples, 0.10 ms spread)
+        // the iteration's live camera samples are counted in the same block reduction (the carried
+        // paths are cnt[0]), on one of kStatLines counters by block (one atomic per block on a single
+        // word capped an empty camera-ray launch at ~88 atomics/us: 1.14 ms for 25.6 M samples, 0.10 ms
+        // spread); launches without camera samples count nothing
         uint32_t* const cs[kClasses] = {&cnt[cix(1)], &cnt[cix(2)], &cnt[cix(3)], &cnt[cix(4)], &cnt[cix(5)]};
-        const uint32_t slot = block_slot<kClasses>(cls, cs, live, &cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))]);
+        const uint32_t slot = block_slot<kClasses>(cls, cs, gen && live,
+                                                   PART == kExtCarried ? nullptr : &cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))]);
         if (cls >= 0) queues[cls][slot] = i;
     }
 }
