@@ -728,6 +728,42 @@ void stage(rs_scene* s, const T*& field, const std::vector<T>& v) {
     s->hs.blobs.push_back(std::move(b));
 }
 
+// The LDS image of a nest-mode scene (DScene::limg): the staged tables a traversal reads, each at a
+// 16-byte aligned offset of one blob, when they fit kLimgMax (quadric.sdl: ~3 KB). The tables stay
+// in their own arrays too (the shading kernels and the other paths read those).
+void build_limg(rs_scene* s) {
+    DScene& d = s->hs.ds;
+    d.limg = nullptr;
+    d.limg_bytes = 0;
+    std::memset(d.limg_off, 0, sizeof(d.limg_off));
+    if (s->scene_mode != kSmNest0 && s->scene_mode != kSmNest2) return;
+    const uint32_t cap = kLimgMax;
+#ifdef RS_DEV_KNOBS
+    if (std::getenv("RS_NO_LIMG")) return;  // the tables in global memory, for comparison
+#endif
+    const void* const* fields[LT_COUNT] = {
+        (const void* const*)&d.nodes4, (const void* const*)&d.pbox, (const void* const*)&d.pclass,
+        (const void* const*)&d.prims, (const void* const*)&d.spheres, (const void* const*)&d.rects,
+        (const void* const*)&d.boxes, (const void* const*)&d.quadrics, (const void* const*)&d.csgs,
+        (const void* const*)&d.xforms, (const void* const*)&d.tf_fwd, (const void* const*)&d.tf_inv};
+    std::vector<char> img;
+    for (int t = 0; t < LT_COUNT; ++t) {
+        const size_t fo = (size_t)((const char*)fields[t] - (const char*)&d);
+        img.resize((img.size() + 15) & ~(size_t)15);
+        d.limg_off[t] = (uint32_t)img.size();
+        for (const Blob& b : s->hs.blobs)
+            if (b.field_off == fo) img.insert(img.end(), b.bytes.begin(), b.bytes.end());
+        if (img.size() > cap) return;
+    }
+    img.resize((img.size() + 15) & ~(size_t)15);
+    if (img.size() > cap) return;
+    d.limg_bytes = (uint32_t)img.size();
+    Blob b;
+    b.field_off = (size_t)((const char*)&d.limg - (const char*)&d);
+    b.bytes = std::move(img);
+    s->hs.blobs.push_back(std::move(b));
+}
+
 // copy the staged scene to `device` as a new replica
 void upload_replica(rs_scene* s, int device) {
     std::unique_ptr<Replica> R(new Replica());
@@ -1062,6 +1098,14 @@ void build(rs_scene* s) {
         }
     }
     d.stack_need = s->stack_need;
+    {
+        uint32_t bits = 1;
+        while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)s->n_nodes) ++bits;
+        d.stk_mask = bits <= 24 ? (uint32_t)(((uint64_t)1 << bits) - 1) : 0xFFFFFFFFu;
+#ifdef RS_DEV_KNOBS
+        if (std::getenv("RS_NO_POPCULL")) d.stk_mask = 0xFFFFFFFFu;  // plain pops, for comparison
+#endif
+    }
     d.moving = 0;
     for (const DSphere& sp : spheres)
         if (sp.v[0] != 0.0 || sp.v[1] != 0.0 || sp.v[2] != 0.0) d.moving = 1;
@@ -1152,6 +1196,7 @@ void build(rs_scene* s) {
     d.ref_order = s->ref_order ? 1 : 0;
     for (int i = 0; i < 3; ++i) { d.bg_lo[i] = s->bg_lo[i]; d.bg_hi[i] = s->bg_hi[i]; }
     d.bg_lo[3] = d.bg_hi[3] = 1.0f;
+    build_limg(s);
 }
 
 // rs_scene_commit / rs_scene_commit_devices: build once, then one replica per listed device

@@ -69,11 +69,21 @@ template <class T>
 __device__ __forceinline__ T gld(const void* base, uint32_t byte_off) {
     return *(const RS_GLOBAL T*)((const RS_GLOBAL char*)base + byte_off);
 }
+// Tree-node loads: global (gld), or with the scene's LDS image (LOBJ, lds_scene) plain loads through
+// the image's pointers, which derive from the __shared__ array: the compiler emits ds_read for them.
+template <bool LOBJ, class T>
+__device__ __forceinline__ T nld(const void* base, uint32_t byte_off) {
+    if constexpr (LOBJ) return *(const T*)((const char*)base + byte_off);
+    else return gld<T>(base, byte_off);
+}
 
 #ifdef RS_TRAV_STATS  // dev builds only (tools/build_variant.sh -DRS_TRAV_STATS): traversal counters
 __device__ unsigned long long g_trav_stats[32];  // [8 + b]: rays with 8b .. 8b+7 node steps (b < 16, last = more)
 #define RS_STAT(k, v) atomicAdd(&g_trav_stats[k], (unsigned long long)(v))
 __shared__ int s_st_nodes[256], s_st_leaves[256], s_st_witer[256];
+// per thread: stack words popped, and popped words dropped by their entry (stk_pop)
+__shared__ int s_st_pops[256], s_st_cull[256];
+__device__ __forceinline__ void st_reset() { s_st_pops[threadIdx.x] = 0; s_st_cull[threadIdx.x] = 0; }
 #endif
 
 // aabb.rs:20-38 with inv = 1/d[i] precomputed per ray (the reference recomputes the same value
@@ -177,13 +187,14 @@ __device__ __forceinline__ bool slab4(float nx, float ny, float nz, float fx, fl
 // boxes, fetched at the per-ray byte offsets of the ray's direction signs, and the child codes. (A 64-byte
 // node with half-float planes, rounded outward, the whole node in four loads and the arrays selected and
 // widened in registers, measured 3 % slower on the bench frame and equal on the C5 mesh: round 4.)
+template <bool LOBJ = false>
 __device__ __forceinline__ void load_node4(const DScene& S, const RayF4& rq, int node, f4v& NX, f4v& FX, f4v& NY, f4v& FY,
                                            f4v& NZ, f4v& FZ, i4v& NC) {
     const uint32_t nb = (uint32_t)node * (uint32_t)sizeof(DNode4);  // < 4 GiB of nodes (host-checked)
-    NX = gld<f4v>(S.nodes4, nb + rq.noff[0]); FX = gld<f4v>(S.nodes4, nb + far_off(rq.noff[0], 0));
-    NY = gld<f4v>(S.nodes4, nb + rq.noff[1]); FY = gld<f4v>(S.nodes4, nb + far_off(rq.noff[1], 1));
-    NZ = gld<f4v>(S.nodes4, nb + rq.noff[2]); FZ = gld<f4v>(S.nodes4, nb + far_off(rq.noff[2], 2));
-    NC = gld<i4v>(S.nodes4, nb + 96u);
+    NX = nld<LOBJ, f4v>(S.nodes4, nb + rq.noff[0]); FX = nld<LOBJ, f4v>(S.nodes4, nb + far_off(rq.noff[0], 0));
+    NY = nld<LOBJ, f4v>(S.nodes4, nb + rq.noff[1]); FY = nld<LOBJ, f4v>(S.nodes4, nb + far_off(rq.noff[1], 1));
+    NZ = nld<LOBJ, f4v>(S.nodes4, nb + rq.noff[2]); FZ = nld<LOBJ, f4v>(S.nodes4, nb + far_off(rq.noff[2], 2));
+    NC = nld<LOBJ, i4v>(S.nodes4, nb + 96u);
 }
 
 // Test one leaf object with the range [tmin, best); on acceptance best := its t1 (the
@@ -308,7 +319,7 @@ __device__ __forceinline__ bool flat_hit(const DScene& S, const DPrim& P, const 
 // AND it hits within [tmin, best). Both are pure, so the cheap test runs first: for spheres the
 // discriminant, for triangles the barycentric test, and the exact box only for those that hit.
 // On acceptance bp := e (traverse maps the winning entry to its prim handle at the end).
-template <int SM>
+template <int SM, bool LOBJ = false>
 __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, const RayC& rc, double tmin, double& best,
                                           double& bend, int& bp) {
     if (SM == kSmSpheres) {  // prim-indexed sphere copy: no DPrim hop (e is the prim in this mode)
@@ -404,6 +415,7 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
     int wi = live ? s_st_witer[threadIdx.x] : 0;  // the wave's leaf-loop passes: the max over its lanes
     for (int off = 32; off > 0; off >>= 1) wi = max(wi, __shfl_xor(wi, off, 64));
     if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); RS_STAT(6, wi); }
+    if (live) { RS_STAT(24, s_st_pops[threadIdx.x]); RS_STAT(25, s_st_cull[threadIdx.x]); }
     if (live) RS_STAT(8 + min(15, s_st_nodes[threadIdx.x] / 8), 1);
 }
 #endif
@@ -417,10 +429,37 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
 #define RS_ST_PARAMS
 #define RS_ST_PASS
 #endif
-template <int SM, class STK>
+// A pushed inner node's stack word: its index in the bits of DScene::stk_mask, the high bits of its
+// entry distance above them (a lower bound of the entry: the float's low bits cleared).
+__device__ __forceinline__ int stk_word(int n, float e, uint32_t m) {
+    return (int)((__float_as_uint(e) & ~m) | (uint32_t)n);
+}
+// Pop the next node whose entry the range can still reach (-1: the stack is empty). A child box passes
+// slab4 only with entry <= min(best32, exits) widened by the 2^-18 slack, at most `lim`; a node's
+// children lie in its box (rounded outward from nested exact boxes), so their entries are >= its own:
+// a node entered beyond lim has no child that passes. (Bench frame: a third of the pops, C5's mesh
+// 29 %: profiles/r4/ab/trav_stats_pop_cull.txt.)
+template <class STK>
+__device__ __forceinline__ int stk_pop(const STK& stk, int& sp, uint32_t m, float best32) {
+    const float lim = fmaf(fabsf(best32), 0x1p-18f, best32);
+    while (sp > 0) {
+        --sp;
+        const uint32_t w = (uint32_t)stk.get(sp);
+#ifdef RS_TRAV_STATS
+        ++s_st_pops[threadIdx.x];
+#endif
+        if (!(__uint_as_float(w & ~m) > lim)) return (int)(w & m);
+#ifdef RS_TRAV_STATS
+        ++s_st_cull[threadIdx.x];
+#endif
+    }
+    return -1;
+}
+
+template <int SM, class STK, bool LOBJ = false>
 __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const RayC& rc, const RayF4& rq, double tmin,
-                                 float tmin32, int node, int& sp, const STK& stk, double& best, double& bend,
-                                 int& bp, float& best32 RS_ST_PARAMS) {
+                                 float tmin32, int node, int& sp, const STK& stk, uint32_t smask, double& best,
+                                 double& bend, int& bp, float& best32 RS_ST_PARAMS) {
 #ifdef RS_TRAV_STATS
 #define RS_ST_LEAF4() ++st_leaves
 #else
@@ -430,12 +469,12 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
     do {                                                                       \
         RS_ST_LEAF4();                                                         \
         const int bp_prev = bp;                                                \
-        test_leaf<SM>(S, ~(code), r, rc, tmin, best, bend, bp);                \
+        test_leaf<SM, LOBJ>(S, ~(code), r, rc, tmin, best, bend, bp);          \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
     f4v NX, FX, NY, FY, NZ, FZ;
     i4v NC;
-    load_node4(S, rq, node, NX, FX, NY, FY, NZ, FZ, NC);
+    load_node4<LOBJ>(S, rq, node, NX, FX, NY, FY, NZ, FZ, NC);
     // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
     // and tested after the four box tests, when the node's registers are dead. Branch-free:
     // all four boxes are tested (the node's loads issue together) and the slot results are
@@ -461,25 +500,23 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #endif
     const int cnt = (e0 > -__builtin_huge_valf()) + (e1 > -__builtin_huge_valf()) +
                     (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
-    int next;
-    if (cnt == 0) {
-        next = -1;
-        if (sp > 0) { --sp; next = stk.get(sp); }
-    } else {
+    int next = -1;
+    if (cnt > 0) {
         // sort descending by entry (farthest first, not-visited last): 5 compare-swaps
 #define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
         RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
 #undef RS_CS
-        // the cnt - 1 farther children are pushed; inside the LDS part all three writes are
-        // issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
+        // the cnt - 1 farther children are pushed (with their entries, stk_word); inside the LDS part
+        // all three writes are issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
+        const int w0 = stk_word(n0, e0, smask), w1 = stk_word(n1, e1, smask), w2 = stk_word(n2, e2, smask);
         if (!STK::kOvf || sp + 3 <= kStackMax) {
-            stk.lds[sp * kBlock] = n0;
-            stk.lds[(sp + 1) * kBlock] = n1;
-            stk.lds[(sp + 2) * kBlock] = n2;
+            stk.lds[sp * kBlock] = w0;
+            stk.lds[(sp + 1) * kBlock] = w1;
+            stk.lds[(sp + 2) * kBlock] = w2;
         } else {
-            if (cnt > 1) stk.put(sp, n0);
-            if (cnt > 2) stk.put(sp + 1, n1);
-            if (cnt > 3) stk.put(sp + 2, n2);
+            if (cnt > 1) stk.put(sp, w0);
+            if (cnt > 2) stk.put(sp + 1, w1);
+            if (cnt > 3) stk.put(sp + 2, w2);
         }
         sp += cnt - 1;
         next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
@@ -497,6 +534,7 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
         else break;
         RS_LEAF4(code);
     }
+    if (cnt == 0) next = stk_pop(stk, sp, smask, best32);  // with the range the leaves left
     return next;
 #undef RS_LEAF4
 #undef RS_ST_LEAF4
@@ -519,7 +557,7 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #define RS_LEAFQ_THR 48  // leaf pass at >= 48/64 of the working lanes with an entry queued
 template <int SM, class STK>
 __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, float tmin32, float best32, int node, int& sp,
-                                           const STK& stk, int* q, int& qt) {
+                                           const STK& stk, uint32_t smask, int* q, int& qt) {
     f4v NX, FX, NY, FY, NZ, FZ;
     i4v NC;
     load_node4(S, rq, node, NX, FX, NY, FY, NZ, FZ, NC);
@@ -551,20 +589,20 @@ __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, flo
                     (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
     int next;
     if (cnt == 0) {
-        next = -1;
-        if (sp > 0) { --sp; next = stk.get(sp); }
+        next = stk_pop(stk, sp, smask, best32);
     } else {
 #define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
         RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
 #undef RS_CS
+        const int w0 = stk_word(n0, e0, smask), w1 = stk_word(n1, e1, smask), w2 = stk_word(n2, e2, smask);
         if (!STK::kOvf || sp + 3 <= kStackMax) {
-            stk.lds[sp * kBlock] = n0;
-            stk.lds[(sp + 1) * kBlock] = n1;
-            stk.lds[(sp + 2) * kBlock] = n2;
+            stk.lds[sp * kBlock] = w0;
+            stk.lds[(sp + 1) * kBlock] = w1;
+            stk.lds[(sp + 2) * kBlock] = w2;
         } else {
-            if (cnt > 1) stk.put(sp, n0);
-            if (cnt > 2) stk.put(sp + 1, n1);
-            if (cnt > 3) stk.put(sp + 2, n2);
+            if (cnt > 1) stk.put(sp, w0);
+            if (cnt > 2) stk.put(sp + 1, w1);
+            if (cnt > 3) stk.put(sp + 2, w2);
         }
         sp += cnt - 1;
         next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
@@ -584,8 +622,10 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
     double best = RS_INF, bend = RS_INF;
     float best32 = __builtin_huge_valf();
     int bp = -1, node = S.root4, sp = 0, qh = 0, qt = 0;
+    const uint32_t smask = S.stk_mask;
 #ifdef RS_TRAV_STATS
     int st_nodes = 0, st_leaves = 0, st_witer = 0;
+    st_reset();
 #endif
     while (true) {
         const bool has_leaf = qt != qh;
@@ -611,7 +651,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
 #ifdef RS_TRAV_STATS
             ++st_nodes;
 #endif
-            node = bvh4_node_q<SM>(S, rq, tmin32, best32, node, sp, stk, q, qt);
+            node = bvh4_node_q<SM>(S, rq, tmin32, best32, node, sp, stk, smask, q, qt);
         }
     }
 #ifdef RS_TRAV_STATS
@@ -626,7 +666,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
 // World::hit, inlined into the kernels of every scene mode (a real call makes the kernel keep its live
 // registers in scratch across it: the nest-2 extend spilled 1.2 KB per lane; the generic mode as a
 // call measured slower in round 3, profiles/r3/ab/generic_inline_*.txt)
-template <int SM, class STK>
+template <int SM, class STK, bool LOBJ = false>
 __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if (S.root < 0) return -1;
     const RayC rc = ray_consts(r);
@@ -639,6 +679,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
     int sp = 0;
 #ifdef RS_TRAV_STATS
     int st_nodes = 0, st_leaves = 0, st_witer = 0;
+    st_reset();
 #define RS_ST_NODE() ++st_nodes
 #define RS_ST_LEAF() ++st_leaves
 #else
@@ -650,7 +691,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
     do {                                                                       \
         RS_ST_LEAF();                                                          \
         const int bp_prev = bp;                                                \
-        test_leaf<SM>(S, ~(code), r, rc, tmin, best, bend, bp);                \
+        test_leaf<SM, LOBJ>(S, ~(code), r, rc, tmin, best, bend, bp);          \
         if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);               \
     } while (0)
     // (the generic mode carries it too: its kernels include the World::hit probe, k_probe_hit, which
@@ -663,7 +704,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
         node = S.root4;
         while (true) {
             const uint32_t nb = (uint32_t)node * (uint32_t)sizeof(DNode4) + 4u * (uint32_t)k;
-            const int c = gld<int>(S.nodes4, nb + 96u);
+            const int c = nld<LOBJ, int>(S.nodes4, nb + 96u);
             if (c == INT32_MIN) {  // slots are filled from the left: the node is done
                 if (sp == 0) break;
                 --sp;
@@ -671,8 +712,10 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
                 node = v >> 2; k = v & 3;
                 continue;
             }
-            const float lo[3] = {gld<float>(S.nodes4, nb), gld<float>(S.nodes4, nb + 16u), gld<float>(S.nodes4, nb + 32u)};
-            const float hi[3] = {gld<float>(S.nodes4, nb + 48u), gld<float>(S.nodes4, nb + 64u), gld<float>(S.nodes4, nb + 80u)};
+            const float lo[3] = {nld<LOBJ, float>(S.nodes4, nb), nld<LOBJ, float>(S.nodes4, nb + 16u),
+                                 nld<LOBJ, float>(S.nodes4, nb + 32u)};
+            const float hi[3] = {nld<LOBJ, float>(S.nodes4, nb + 48u), nld<LOBJ, float>(S.nodes4, nb + 64u),
+                                 nld<LOBJ, float>(S.nodes4, nb + 80u)};
             float e;
             if (slab32(lo, hi, rf, tmin32, best32, e)) {
                 RS_ST_NODE();
@@ -694,10 +737,11 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
     } else if (S.root4 >= 0 && !S.ref_order) {
         // 4-wide near-first (bvh4_step): nearest inner child next, the rest pushed far-to-near
         const RayF4 rq = make_rayf4(rf);
+        const uint32_t smask = S.stk_mask;
         node = S.root4;
         while (node >= 0) {
             RS_ST_NODE();
-            node = bvh4_step<SM>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
+            node = bvh4_step<SM, STK, LOBJ>(S, r, rc, rq, tmin, tmin32, node, sp, stk, smask, best, bend, bp, best32 RS_ST_PASS);
         }
     } else if ((SM == kSmSpheres || SM == kSmFlat || SM == kSmGeneric) && !S.ref_order) {
         // binary near-first (monotone scenes without the 4-wide tree); the nest modes use the
@@ -1254,16 +1298,51 @@ constexpr int kClsLight = 6;
 // 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 2 (unbounded, the camera part took
 // 2 AGPRs beyond 256 VGPRs: one wave per SIMD; 3 waves spilled 288 B)
 constexpr int ext_min_waves(int sm) { return sm == kSmNest2 ? 2 : 4; }
+
+// The scene's LDS image (DScene::limg, nest modes): the block copies it into its dynamic LDS and
+// reads the tree and the object tables through a DScene copy whose table pointers point there.
+// The copy is a by-value aggregate used only by inlined code, so it stays in SGPRs, and the
+// compiler sees the tables' LDS origin (ds_read). The node -> prim -> CSG -> child -> shape
+// chain of a nested-object test becomes LDS round trips instead of L1 / L2 ones.
+extern __shared__ uint4 s_limg[];
+// fill the block's copy of the image; every thread of the block calls it (barrier)
+__device__ __forceinline__ void lds_fill(const DScene& Sv) {
+    const uint32_t nq = Sv.limg_bytes >> 4;
+    const uint4* __restrict__ src = (const uint4*)Sv.limg;
+    for (uint32_t q = threadIdx.x; q < nq; q += kBlock) s_limg[q] = src[q];
+    __syncthreads();
+}
+// Sv := the scene with its table pointers into the LDS copy (fill: also fill the copy)
+__device__ __forceinline__ void lds_scene(const DScene* __restrict__ Sp, DScene& Sv, bool fill = true) {
+    Sv = *Sp;
+    if (fill) lds_fill(Sv);
+    const char* b = (const char*)s_limg;
+    Sv.nodes4 = (const DNode4*)(b + Sv.limg_off[LT_NODES4]);
+    Sv.pclass = (const uint8_t*)(b + Sv.limg_off[LT_PCLASS]);
+    Sv.pbox = (const DBox64*)(b + Sv.limg_off[LT_PBOX]);
+    Sv.prims = (const DPrim*)(b + Sv.limg_off[LT_PRIMS]);
+    Sv.spheres = (const DSphere*)(b + Sv.limg_off[LT_SPHERES]);
+    Sv.rects = (const DRect*)(b + Sv.limg_off[LT_RECTS]);
+    Sv.boxes = (const DBox*)(b + Sv.limg_off[LT_BOXES]);
+    Sv.quadrics = (const DQuadric*)(b + Sv.limg_off[LT_QUADRICS]);
+    Sv.csgs = (const DCsg*)(b + Sv.limg_off[LT_CSGS]);
+    Sv.xforms = (const DXform*)(b + Sv.limg_off[LT_XFORMS]);
+    Sv.tf_fwd = (const DMat34*)(b + Sv.limg_off[LT_TF_FWD]);
+    Sv.tf_inv = (const DMat34*)(b + Sv.limg_off[LT_TF_INV]);
+}
 // PART (rs_internal.h): kExtAll -- the carried paths and the injected camera samples in one launch;
 // kExtCarried / kExtCamera -- one of the two (an iteration then takes two launches): where the merged
 // kernel needs more registers than either alone (nest-2: 256 VGPRs + 2 AGPRs, one wave per SIMD,
 // against two waves for each part)
-template <int SM, bool OVF, int PART>
+// LOBJ: the scene's tables from its LDS image (lds_scene; the launch passes limg_bytes of dynamic LDS)
+template <int SM, bool OVF, int PART, bool LOBJ>
 __global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W,
                                                                           uint32_t* const* __restrict__ queues, uint32_t it,
                                                                           double* __restrict__ rad, DCamera C, PathParams P,
                                                                           InjParams I) {
-    const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
+    DScene Sv;
+    if constexpr (LOBJ) lds_scene(Sp, Sv, false);  // filled in the first pass of the loop below
+    const DScene& S = LOBJ ? Sv : *Sp;  // otherwise the scene in device memory (no by-value copy in scratch)
     __shared__ int stk_all[kStackMax * kBlock];
     const StkT<OVF> stk = make_stk<OVF>(S, stk_all);
     uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
@@ -1280,10 +1359,10 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const 
         const uint32_t i = gen ? nf + (j - n_old) : j < nf ? j : W.cap - 1u - (j - nf);
         int cls = -1;
         bool live = false;
+        Ray r;
+        Rng rng;
+        uint32_t item = 0;
         if (j < n) {
-            Ray r;
-            Rng rng;
-            uint32_t item = 0;
             if (gen) {
                 uint32_t jb = I.jb0 + (j - n_old), nb = I.nb0;
                 uint64_t g0 = I.g0;
@@ -1297,57 +1376,61 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const 
                 r = load_ray(cur, i);
                 live = true;
             }
-            if (live) {
-                double bend = RS_INF;
-                const int bp = traverse<SM>(S, r, 0.0001, bend, stk);
-                V3 add;
-                bool done = true;
-                if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
-                    add = background(S, r);
-                } else {
-                    cls = (int)S.pclass[bp];
-                    if (cls == kClsLight) {  // DiffuseLight: emitted, scatter None (camera.rs:172-176,250)
-                        Hit h;
-                        int mi;
-                        if (SM == kSmSpheres) {
-                            const DPrim Pr = S.prims[bp];
-                            sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
-                            mi = Pr.mat;
+        }
+        // the LDS image is filled once the block's first records are requested: their latency and the
+        // image's overlap at the barrier
+        if constexpr (LOBJ)
+            if (base == blockIdx.x * kBlock) lds_fill(S);
+        if (live) {
+            double bend = RS_INF;
+            const int bp = traverse<SM, StkT<OVF>, LOBJ>(S, r, 0.0001, bend, stk);
+            V3 add;
+            bool done = true;
+            if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
+                add = background(S, r);
+            } else {
+                cls = (int)S.pclass[bp];
+                if (cls == kClsLight) {  // DiffuseLight: emitted, scatter None (camera.rs:172-176,250)
+                    Hit h;
+                    int mi;
+                    if (SM == kSmSpheres) {
+                        const DPrim Pr = S.prims[bp];
+                        sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
+                        mi = Pr.mat;
+                    } else {
+                        // emission reads the record's material and point only: for a leaf object
+                        // (a light class is only given to leaf objects and TfFacades of them) from
+                        // its t-only test, without inlining the nested-object code a second time
+                        if (S.prims[bp].kind != PK_XFORM) {
+                            HitT ht;
+                            Obj<0, 0>::hit_t(S, bp, r, 0.0001, bend, ht);
+                            h.p = ht.p;
+                            mi = S.prims[bp].mat;
                         } else {
-                            // emission reads the record's material and point only: for a leaf object
-                            // (a light class is only given to leaf objects and TfFacades of them) from
-                            // its t-only test, without inlining the nested-object code a second time
-                            if (S.prims[bp].kind != PK_XFORM) {
-                                HitT ht;
-                                Obj<0, 0>::hit_t(S, bp, r, 0.0001, bend, ht);
-                                h.p = ht.p;
-                                mi = S.prims[bp].mat;
-                            } else {
-                                finish_hit<SM>(S, bp, r, 0.0001, bend, h);
-                                mi = h.mat;
-                            }
+                            finish_hit<SM>(S, bp, r, 0.0001, bend, h);
+                            mi = h.mat;
                         }
-                        add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
-                        cls = -1;
-                    } else {
-                        W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-                        // a camera sample that goes on to shading: its record (T = 1, level 0); a carried
-                        // path's is in place
-                        if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
-                        done = false;
                     }
+                    add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
+                    cls = -1;
+                } else {
+                    W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+                    // a camera sample that goes on to shading: its record (T = 1, level 0); a carried
+                    // path's is in place
+                    if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
+                    done = false;
                 }
-                if (done) {  // 0 + T * add: the path's radiance so far is 0 (WfSet)
-                    D4 t4;
-                    if (gen) {
-                        t4.x = t4.y = t4.z = 1.0;
-                    } else {
-                        t4 = cur.thr[i]; item = cur.tag[i].x;
-                    }
-                    rad[item] = 0.0 + t4.x * add.x;
-                    rad[I.ring + item] = 0.0 + t4.y * add.y;
-                    rad[2 * I.ring + item] = 0.0 + t4.z * add.z;
+            }
+            if (done) {  // 0 + T * add: the path's radiance so far is 0 (WfSet)
+                D4 t4;
+                if (gen) {
+                    t4.x = t4.y = t4.z = 1.0;
+                } else {
+                    t4 = cur.thr[i]; item = cur.tag[i].x;
                 }
+                rad[item] = 0.0 + t4.x * add.x;
+                rad[I.ring + item] = 0.0 + t4.y * add.y;
+                rad[2 * I.ring + item] = 0.0 + t4.z * add.z;
             }
         }
 #ifdef RS_TRAV_STATS
@@ -1432,15 +1515,17 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // runs its class's specialised code. One launch per iteration instead of one per class removes the
 // per-class launch tails (the small classes' queues take 5-50 us each however short they are).
 // G4: the scene has class-4 prims (the generic material switch, composite objects), compiled in only
-// then (it sets the kernel's register count).
-template <int SM, bool G4>
+// then (it sets the kernel's register count). LOBJ: the scene's tables from its LDS image (lds_scene).
+template <int SM, bool G4, bool LOBJ>
 __global__ __launch_bounds__(kBlock, SM == kSmNest2 ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
                                                                                    double* __restrict__ rad) {
     // (3 waves: 171 -> 168 VGPRs; at 4 waves it spilled 156 B, +6 %; nest-2 bounded at 3 spilled: C4 -21 %)
-    const DScene& S = *Sp;
+    DScene Sv;
+    if constexpr (LOBJ) lds_scene(Sp, Sv);
+    const DScene& S = LOBJ ? Sv : *Sp;
     const uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
     uint32_t* cnt_next = W.counts + (size_t)(it + 1) * kWfsStride;
     constexpr int NC = G4 ? 5 : 4;
@@ -1706,12 +1791,20 @@ hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& 
                          uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, int part, hipStream_t st,
                          hipEvent_t ev0, hipEvent_t ev1) {
     if (!blocks) return hipSuccess;
-#define RS_EXT_LAUNCH(OVF, PART)                                                                                   \
-    hipExtLaunchKernelGGL((k_wfs_extend<SMC, OVF, PART>), dim3(blocks), dim3(kBlock), 0, st, ev0, ev1, 0, s.dev, w, \
-                          queues, it, rad, c, p, inj)
+#define RS_EXT_LAUNCH(OVF, PART) RS_EXT_LAUNCH_L(OVF, PART, false, 0)
+#define RS_EXT_LAUNCH_L(OVF, PART, LOBJ, SHM)                                                                        \
+    hipExtLaunchKernelGGL((k_wfs_extend<SMC, OVF, PART, LOBJ>), dim3(blocks), dim3(kBlock), SHM, st, ev0, ev1, 0, s.dev, \
+                          w, queues, it, rad, c, p, inj)
+    // nest modes: the LDS image when the scene has one (the spheres mode has none: its 41 KB tree and
+    // sphere records per block halved the extend's occupancy, bench frame 7.63 -> 9.94 ms)
+    const uint32_t shm = s.host->limg_bytes;
     if constexpr (SMC == kSmNest2) {  // split launches only (ext_split)
-        if (part == kExtCamera) RS_EXT_LAUNCH(true, kExtCamera);
-        else RS_EXT_LAUNCH(true, kExtCarried);
+        if (part == kExtCamera) { if (shm) RS_EXT_LAUNCH_L(true, kExtCamera, true, shm); else RS_EXT_LAUNCH(true, kExtCamera); }
+        else { if (shm) RS_EXT_LAUNCH_L(true, kExtCarried, true, shm); else RS_EXT_LAUNCH(true, kExtCarried); }
+    } else if constexpr (SMC == kSmNest0) {
+        if (part == kExtAll) { if (shm) RS_EXT_LAUNCH_L(true, kExtAll, true, shm); else RS_EXT_LAUNCH(true, kExtAll); }
+        else if (part == kExtCamera) { if (shm) RS_EXT_LAUNCH_L(true, kExtCamera, true, shm); else RS_EXT_LAUNCH(true, kExtCamera); }
+        else { if (shm) RS_EXT_LAUNCH_L(true, kExtCarried, true, shm); else RS_EXT_LAUNCH(true, kExtCarried); }
     } else if constexpr (SMC == kSmSpheres) {
         const bool lds = lds_only_stack(s);
         if (part == kExtAll) { if (lds) RS_EXT_LAUNCH(false, kExtAll); else RS_EXT_LAUNCH(true, kExtAll); }
@@ -1723,6 +1816,7 @@ hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& 
         else RS_EXT_LAUNCH(true, kExtCarried);
     }
 #undef RS_EXT_LAUNCH
+#undef RS_EXT_LAUNCH_L
     return hipGetLastError();
 }
 
@@ -1730,12 +1824,18 @@ template <int SMC>
 hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, uint32_t it,
                             uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, hipStream_t st) {
     if (!blocks) return hipSuccess;
-    if (class_mask & (1u << 4))
-        hipLaunchKernelGGL((k_wfs_shade_all<SMC, true>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues, class_mask, it,
-                           depth, ring, rad);
-    else
-        hipLaunchKernelGGL((k_wfs_shade_all<SMC, false>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, queues, class_mask, it,
-                           depth, ring, rad);
+#define RS_SHADE_LAUNCH(G4, LOBJ, SHM)                                                                              \
+    hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, queues, class_mask, \
+                       it, depth, ring, rad)
+    const uint32_t shm = s.host->limg_bytes;  // nest modes' LDS image (none in the spheres mode)
+    if constexpr (SMC == kSmNest0 || SMC == kSmNest2) {
+        if (class_mask & (1u << 4)) { if (shm) RS_SHADE_LAUNCH(true, true, shm); else RS_SHADE_LAUNCH(true, false, 0); }
+        else { if (shm) RS_SHADE_LAUNCH(false, true, shm); else RS_SHADE_LAUNCH(false, false, 0); }
+    } else {
+        if (class_mask & (1u << 4)) RS_SHADE_LAUNCH(true, false, 0);
+        else RS_SHADE_LAUNCH(false, false, 0);
+    }
+#undef RS_SHADE_LAUNCH
     return hipGetLastError();
 }
 #endif  // RS_TU_MODES

@@ -155,6 +155,13 @@ struct DBox64 {    // an object's reference bbox (exact f64), tested before its 
     double hi[3];
 };
 
+// tables of the LDS image (DScene::limg_off), in image order
+enum LimgTable { LT_NODES4 = 0, LT_PBOX, LT_PCLASS, LT_PRIMS, LT_SPHERES, LT_RECTS, LT_BOXES, LT_QUADRICS, LT_CSGS,
+                 LT_XFORMS, LT_TF_FWD, LT_TF_INV, LT_COUNT };
+// LDS bytes the image may take: the nest-0 extend keeps 4 blocks of 256 per CU, each with its
+// 24 KiB traversal stack (4 x (24 + 15) KiB <= 160 KiB)
+constexpr uint32_t kLimgMax = 15u * 1024u;
+
 struct DScene {
     const DNode* nodes;      // binary tree (reference-order scenes)
     const DNode4* nodes4;    // 4-wide tree (monotone scenes), root = root4
@@ -186,6 +193,13 @@ struct DScene {
     // column (blockIdx.x * kBlock + threadIdx.x) of a [stack_need - kStackMax][gridDim.x * kBlock]
     // array that the host sizes per launch grid (null when the tree fits the LDS stack).
     int32_t* stk_ovf;
+    // Nest modes: the small tables a traversal reads (4-wide tree, own boxes, classes, object records)
+    // as one image that the extend's blocks copy into LDS (rs_kernels.hip lds_scene), so the dependent
+    // node -> prim -> CSG -> child -> shape loads of a nested-object test are LDS reads. Null (and
+    // limg_bytes 0) when the scene's tables exceed kLimgMax.
+    const void* limg;
+    uint32_t limg_bytes;                  // a multiple of 16
+    uint32_t limg_off[LT_COUNT];          // byte offset of each table in the image (LimgTable order)
     int32_t n_lights;
     int32_t root;            // root child code (node index, or ~prim if a single object, or INT32_MIN if empty)
     int32_t default_mat;     // world.rs:51 Lambertian(Color(1,1,1,1))
@@ -194,6 +208,10 @@ struct DScene {
     int32_t uv;              // 1: hit records carry (u, v) (some texture reads them: Image)
     int32_t has_media;       // 1: the scene has ConstantMedium objects (rays carry the medium key)
     int32_t stack_need;      // exact worst-case traversal stack depth of the tree in use (host-computed)
+    // 4-wide near-first stacks: a pushed node's word carries its entry distance in the bits above its
+    // index (the f32 entry's high bits: a lower bound), so a pop can drop a node the range has passed
+    // by. stk_mask = the index bits (2^k - 1 for 2^k >= nodes); all ones (no entry bits) above 2^24 nodes.
+    uint32_t stk_mask;
     int32_t moving;          // 1: some sphere has a nonzero speed (center_at needs the time)
     float bg_lo[4], bg_hi[4];
 };
