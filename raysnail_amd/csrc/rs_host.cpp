@@ -737,6 +737,9 @@ void build_limg(rs_scene* s) {
     d.limg_bytes = 0;
     std::memset(d.limg_off, 0, sizeof(d.limg_off));
     if (s->scene_mode != kSmNest0 && s->scene_mode != kSmNest2) return;
+    // the image's kernels walk the in-order 4-wide tree with their leaf list in the LDS stack's top
+    // kLeafBatch entries (rs_kernels.hip traverse_deferred)
+    if (d.root4 < 0 || !d.ref_order || s->stack_need + (int)kLeafBatch > kStackMax) return;
     const uint32_t cap = kLimgMax;
 #ifdef RS_DEV_KNOBS
     if (std::getenv("RS_NO_LIMG")) return;  // the tables in global memory, for comparison

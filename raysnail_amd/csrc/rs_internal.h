@@ -10,6 +10,9 @@ constexpr int kBlock = 256;      // 4 waves of 64
 // per-thread BVH stack entries held in LDS (24 KiB/block -> 6 blocks/CU); deeper entries spill to
 // DScene::stk_ovf, which the host sizes from the tree's exact worst-case stack depth
 constexpr int kStackMax = 24;
+// leaves listed per walk by the deferred reference-order traversal (LDS-image scenes), in the top
+// kLeafBatch entries of the thread's LDS stack column
+constexpr uint32_t kLeafBatch = 8;
 constexpr uint32_t kMaxLanes = 4;   // chunk lanes of the bounce-synchronous wavefront (flat / rich scenes)
 constexpr uint32_t kMaxSlots = 4;   // frames in flight per replica (rs_scene_set_frames_in_flight)
 

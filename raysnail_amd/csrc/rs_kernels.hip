@@ -663,12 +663,81 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
     return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
+// World::hit in BVH::hit's recursion order (bvh.rs:173-192) on the in-order 4-wide tree with the leaf
+// tests taken out of the walk: the walk lists the leaves whose boxes the ray reaches in [tmin, inf), in
+// the recursion's order, kLeafBatch at a time into the top of the thread's LDS stack column, and the
+// listed leaves are then tested in that order with the range so far. Same hits as the interleaved walk:
+// the range only culls (a leaf is accepted iff its own exact box passes with the range of its turn and
+// it hits, and the walk's order does not depend on the range), and the list holds every leaf the
+// interleaved walk would test, in order. The walk's and the tests' registers are never live together.
+// A ray with more leaves walks again
+// for the next kLeafBatch (the LDS-image scenes' trees are a few nodes). The host gives a scene its LDS
+// image only when stack_need + kLeafBatch <= kStackMax and the tree is the in-order 4-wide one.
+template <int SM, class STK>
+__device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
+    constexpr uint32_t K = kLeafBatch;
+    int* const q = stk.lds + (kStackMax - (int)K) * kBlock;  // this thread's list slots
+    const RayC rc = ray_consts(r);
+    const float tmin32 = -round_up_f(-tmin);
+    double best = RS_INF, bend = RS_INF;
+    int bp = -1;
+    uint32_t skip = 0;
+    while (true) {
+        uint32_t found = 0;  // leaves met by this walk; slots skip .. skip + K - 1 are listed
+        {
+            const RayF rf = make_rayf(r.o, rc.inv);
+            int k = 0, node = S.root4, sp = 0;
+            while (true) {
+                const uint32_t nb = (uint32_t)node * (uint32_t)sizeof(DNode4) + 4u * (uint32_t)k;
+                const int c = nld<true, int>(S.nodes4, nb + 96u);
+                if (c == INT32_MIN) {  // slots are filled from the left: the node is done
+                    if (sp == 0) break;
+                    --sp;
+                    const int v = stk.get(sp);
+                    node = v >> 2; k = v & 3;
+                    continue;
+                }
+                const float lo[3] = {nld<true, float>(S.nodes4, nb), nld<true, float>(S.nodes4, nb + 16u),
+                                     nld<true, float>(S.nodes4, nb + 32u)};
+                const float hi[3] = {nld<true, float>(S.nodes4, nb + 48u), nld<true, float>(S.nodes4, nb + 64u),
+                                     nld<true, float>(S.nodes4, nb + 80u)};
+                float e;
+                if (slab32(lo, hi, rf, tmin32, __builtin_huge_valf(), e)) {
+                    if (c < 0) {
+                        if (found >= skip && found - skip < K) q[(found - skip) * kBlock] = c;
+                        ++found;
+                    } else {
+                        if (k < 3) { stk.put(sp, node * 4 + k + 1); ++sp; }  // come back for the next slot
+                        node = c;
+                        k = 0;
+                        continue;
+                    }
+                }
+                if (k < 3) { ++k; continue; }
+                if (sp == 0) break;
+                --sp;
+                const int v = stk.get(sp);
+                node = v >> 2; k = v & 3;
+            }
+        }
+        const uint32_t m = found > skip ? min(found - skip, K) : 0u;
+        for (uint32_t i = 0; i < m; ++i) test_leaf<SM, true>(S, ~q[i * kBlock], r, rc, tmin, best, bend, bp);
+        if (found <= skip + K) break;
+        skip += K;
+    }
+    bend_out = bend;
+    return bp;  // nest modes' leaf codes name prims (no lprim)
+}
+
 // World::hit, inlined into the kernels of every scene mode (a real call makes the kernel keep its live
 // registers in scratch across it: the nest-2 extend spilled 1.2 KB per lane; the generic mode as a
 // call measured slower in round 3, profiles/r3/ab/generic_inline_*.txt)
 template <int SM, class STK, bool LOBJ = false>
 __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if (S.root < 0) return -1;
+    // nest-0 only: on nest-2 (C4's scene) the split walk measured 2 % slower, on nest-0 (example.sdl)
+    // 2.5 % faster (profiles/r4/ab/deferred_leaves)
+    if constexpr (LOBJ && SM == kSmNest0) return traverse_deferred<SM>(S, r, tmin, bend_out, stk);
     const RayC rc = ray_consts(r);
     const RayF rf = make_rayf(r.o, rc.inv);
     const float tmin32 = -round_up_f(-tmin);
@@ -807,10 +876,32 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
     return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
-// Recompute the full record of the winner with the exact range it was accepted under.
-template <int SM>
+// The record of a leaf object or of a TfFacade chain over one (tf_facade.rs:41-55): Obj::hit without
+// the CSG code. The material classes 0-3 hold only such prims (rs_host.cpp class_of: composites are
+// class 4), so their shading batches take this smaller finish.
+template <int L>
+__device__ __forceinline__ bool leafish_hit(const DScene& S, int pi, const Ray& r, double tmin, double tmax, Hit& h) {
+    if constexpr (L > 0) {
+        const DPrim P = S.prims[pi];
+        if (P.kind == PK_XFORM) {
+            const DXform X = S.xforms[P.idx];
+            Ray rr = r;
+            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
+            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
+            if (!leafish_hit<L - 1>(S, X.child, rr, tmin, tmax, h)) return false;
+            h.p = tf_forward(S, X, P.aux, h.p, 1.0);
+            return true;
+        }
+    }
+    return Obj<0, 0>::hit(S, pi, r, tmin, tmax, h);
+}
+
+// Recompute the full record of the winner with the exact range it was accepted under. LEAFISH: the
+// prim is a leaf or a TfFacade chain over one (leafish_hit).
+template <int SM, bool LEAFISH = false>
 __device__ __forceinline__ bool finish_hit(const DScene& S, int bp, const Ray& r, double tmin, double bend, Hit& h) {
     if (bp < 0) return false;
+    if constexpr (LEAFISH && (SM == kSmNest0 || SM == kSmNest2)) return leafish_hit<nest_of(SM)>(S, bp, r, tmin, bend, h);
     if ((SM == kSmSpheres) || S.prims[bp].kind == PK_SPHERE) {
         const DPrim P = S.prims[bp];
         return sphere_hit(S.spheres[P.idx], P.mat, r, tmin, bend, h, rich_of(SM) ? S.uv : 0);
@@ -1469,7 +1560,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
         const double2 hb = W.hit[i];
         const int bp = (int)__double_as_longlong(hb.x);
         Hit h;
-        finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
+        finish_hit<SM, (KIND >= 0)>(S, bp, r, 0.0001, hb.y, h);
         const uint2 tg = cur.tag[i];
         item = tg.x;
         lvl = tg.y;
@@ -1517,7 +1608,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // G4: the scene has class-4 prims (the generic material switch, composite objects), compiled in only
 // then (it sets the kernel's register count). LOBJ: the scene's tables from its LDS image (lds_scene).
 template <int SM, bool G4, bool LOBJ>
-__global__ __launch_bounds__(kBlock, SM == kSmNest2 ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
+__global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4) ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
