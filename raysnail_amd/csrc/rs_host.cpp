@@ -576,8 +576,13 @@ int32_t build_ref(std::vector<HNode>& nodes, LeafSink& leaves, std::vector<RefIt
 
 // Collapse the binary tree into a 4-wide one: repeatedly open the inner child with the largest
 // box surface until four slots are filled.
-struct HNode4 { double lo[4][3], hi[4][3]; int32_t child[4]; };
-int32_t collapse4(const std::vector<HNode>& bn, int32_t code, std::vector<HNode4>& out, int depth, int& max_depth) {
+template <int W> struct HNodeW { double lo[W][3], hi[W][3]; int32_t child[W]; };
+using HNode4 = HNodeW<4>;
+// Near-first trees: a node's slots are its binary subtree's top, the largest-area inner slot opened
+// into its two children until W slots are filled (or only leaves remain). (An 8-wide tree for the
+// spheres mode measured slower: profiles/r4/ab/bvh8.)
+template <int W>
+int32_t collapseW(const std::vector<HNode>& bn, int32_t code, std::vector<HNodeW<W>>& out, int depth, int& max_depth) {
     if (code < 0) return code;
     max_depth = std::max(max_depth, depth + 1);
     struct Slot { double lo[3], hi[3]; int32_t c; };
@@ -588,7 +593,7 @@ int32_t collapse4(const std::vector<HNode>& bn, int32_t code, std::vector<HNode4
         for (int a = 0; a < 3; ++a) { sl.lo[a] = n.lo[k][a]; sl.hi[a] = n.hi[k][a]; }
         if (sl.c != INT32_MIN) slots.push_back(sl);
     }
-    while (slots.size() < 4) {
+    while (slots.size() < (size_t)W) {
         int best = -1; double best_area = -1;
         for (size_t i = 0; i < slots.size(); ++i) {
             if (slots[i].c < 0) continue;
@@ -607,10 +612,10 @@ int32_t collapse4(const std::vector<HNode>& bn, int32_t code, std::vector<HNode4
     }
     const int32_t idx = (int32_t)out.size();
     out.emplace_back();
-    int32_t kids[4];
-    for (int k = 0; k < 4; ++k) kids[k] = (size_t)k < slots.size() ? collapse4(bn, slots[k].c, out, depth + 1, max_depth) : INT32_MIN;
-    HNode4& o = out[idx];
-    for (int k = 0; k < 4; ++k) {
+    int32_t kids[W];
+    for (int k = 0; k < W; ++k) kids[k] = (size_t)k < slots.size() ? collapseW<W>(bn, slots[k].c, out, depth + 1, max_depth) : INT32_MIN;
+    HNodeW<W>& o = out[idx];
+    for (int k = 0; k < W; ++k) {
         o.child[k] = kids[k];
         for (int q = 0; q < 3; ++q) {
             o.lo[k][q] = (size_t)k < slots.size() ? slots[k].lo[q] : INFINITY;
@@ -674,15 +679,17 @@ int32_t collapse4_inorder(const std::vector<HNode>& bn, int32_t code, std::vecto
 // Exact worst-case stack depth of traverse() (rs_kernels.hip) over a tree: the most entries any
 // root-to-node path can leave on the stack.
 //  4-wide near-first: a node pushes (inner children hit) - 1 <= (inner children) - 1 entries;
-int stack_need4(const std::vector<HNode4>& n4, int32_t code) {
+template <int W>
+int stack_needW(const std::vector<HNodeW<W>>& n4, int32_t code) {
     if (code < 0) return 0;
     int inner = 0, deepest = 0;
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < W; ++k) {
         const int32_t c = n4[code].child[k];
-        if (c >= 0) { ++inner; deepest = std::max(deepest, stack_need4(n4, c)); }
+        if (c >= 0) { ++inner; deepest = std::max(deepest, stack_needW<W>(n4, c)); }
     }
     return std::max(inner - 1, 0) + deepest;
 }
+int stack_need4(const std::vector<HNode4>& n4, int32_t code) { return stack_needW<4>(n4, code); }
 //  4-wide reference order: the node (with its next slot) when an inner child before slot 3 is entered;
 int stack_need4_ref(const std::vector<HNode4>& n4, int32_t code) {
     if (code < 0) return 0;
@@ -1068,7 +1075,7 @@ void build(rs_scene* s) {
     if (!s->ref_order && root >= 0 && !no_bvh4) {
         std::vector<HNode4> n4;
         int depth4 = 0;
-        const int32_t r4 = collapse4(B.nodes, root, n4, 0, depth4);
+        const int32_t r4 = collapseW<4>(B.nodes, root, n4, 0, depth4);
         if (r4 >= 0) {
             // the kernels address nodes with 32-bit byte offsets (rs_kernels.hip gld)
             if (n4.size() * sizeof(DNode4) > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "scene too large: 4-wide tree over 4 GiB");

@@ -540,6 +540,7 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #undef RS_ST_LEAF4
 }
 
+
 // ---- flat scenes (meshes): node steps and leaf tests in separate wave passes ----
 // In bvh4_step a wave runs each node's leaf loop as long as the lane with the most leaves there, and
 // its other lanes idle through the f64 triangle tests (the lanes' divergence sits inside the node
