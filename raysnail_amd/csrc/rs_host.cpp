@@ -1108,14 +1108,6 @@ void build(rs_scene* s) {
         }
     }
     d.stack_need = s->stack_need;
-    {
-        uint32_t bits = 1;
-        while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)s->n_nodes) ++bits;
-        d.stk_mask = bits <= 24 ? (uint32_t)(((uint64_t)1 << bits) - 1) : 0xFFFFFFFFu;
-#ifdef RS_DEV_KNOBS
-        if (std::getenv("RS_NO_POPCULL")) d.stk_mask = 0xFFFFFFFFu;  // plain pops, for comparison
-#endif
-    }
     d.moving = 0;
     for (const DSphere& sp : spheres)
         if (sp.v[0] != 0.0 || sp.v[1] != 0.0 || sp.v[2] != 0.0) d.moving = 1;
@@ -1795,10 +1787,12 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                     ++path_launches;
                     for (uint32_t b = 0; b < D; ++b) {
                         if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
-                        // meshes: one block per 256 paths (C5 49.6 -> 48.1 ms); the rich mode a bounded grid
+                        // meshes: one block per 256 paths (C5 49.6 -> 48.1 ms), at most 64 per CU where the tree
+                        // spills its stack to HBM (the overflow array is sized for that grid; a grid of resident
+                        // blocks only, grid-striding, made the C5 extend 35 % slower); the rich mode a bounded grid
+                        const uint32_t bn = (n + kBlock - 1) / kBlock;
                         HIP_OK(launch_wf_extend(ds, WS, b,
-                                                sm == kSmFlat && !ext_spill ? (n + kBlock - 1) / kBlock
-                                                                            : std::min(ext_blocks, (n + kBlock - 1) / kBlock),
+                                                sm == kSmFlat ? (ext_spill ? std::min(wide, bn) : bn) : std::min(ext_blocks, bn),
                                                 sm, cs));
                         if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
                         ++ki;

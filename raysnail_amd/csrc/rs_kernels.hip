@@ -81,9 +81,6 @@ __device__ __forceinline__ T nld(const void* base, uint32_t byte_off) {
 __device__ unsigned long long g_trav_stats[32];  // [8 + b]: rays with 8b .. 8b+7 node steps (b < 16, last = more)
 #define RS_STAT(k, v) atomicAdd(&g_trav_stats[k], (unsigned long long)(v))
 __shared__ int s_st_nodes[256], s_st_leaves[256], s_st_witer[256];
-// per thread: stack words popped, and popped words dropped by their entry (stk_pop)
-__shared__ int s_st_pops[256], s_st_cull[256];
-__device__ __forceinline__ void st_reset() { s_st_pops[threadIdx.x] = 0; s_st_cull[threadIdx.x] = 0; }
 #endif
 
 // aabb.rs:20-38 with inv = 1/d[i] precomputed per ray (the reference recomputes the same value
@@ -415,7 +412,6 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
     int wi = live ? s_st_witer[threadIdx.x] : 0;  // the wave's leaf-loop passes: the max over its lanes
     for (int off = 32; off > 0; off >>= 1) wi = max(wi, __shfl_xor(wi, off, 64));
     if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); RS_STAT(6, wi); }
-    if (live) { RS_STAT(24, s_st_pops[threadIdx.x]); RS_STAT(25, s_st_cull[threadIdx.x]); }
     if (live) RS_STAT(8 + min(15, s_st_nodes[threadIdx.x] / 8), 1);
 }
 #endif
@@ -429,37 +425,10 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
 #define RS_ST_PARAMS
 #define RS_ST_PASS
 #endif
-// A pushed inner node's stack word: its index in the bits of DScene::stk_mask, the high bits of its
-// entry distance above them (a lower bound of the entry: the float's low bits cleared).
-__device__ __forceinline__ int stk_word(int n, float e, uint32_t m) {
-    return (int)((__float_as_uint(e) & ~m) | (uint32_t)n);
-}
-// Pop the next node whose entry the range can still reach (-1: the stack is empty). A child box passes
-// slab4 only with entry <= min(best32, exits) widened by the 2^-18 slack, at most `lim`; a node's
-// children lie in its box (rounded outward from nested exact boxes), so their entries are >= its own:
-// a node entered beyond lim has no child that passes. (Bench frame: a third of the pops, C5's mesh
-// 29 %: profiles/r4/ab/trav_stats_pop_cull.txt.)
-template <class STK>
-__device__ __forceinline__ int stk_pop(const STK& stk, int& sp, uint32_t m, float best32) {
-    const float lim = fmaf(fabsf(best32), 0x1p-18f, best32);
-    while (sp > 0) {
-        --sp;
-        const uint32_t w = (uint32_t)stk.get(sp);
-#ifdef RS_TRAV_STATS
-        ++s_st_pops[threadIdx.x];
-#endif
-        if (!(__uint_as_float(w & ~m) > lim)) return (int)(w & m);
-#ifdef RS_TRAV_STATS
-        ++s_st_cull[threadIdx.x];
-#endif
-    }
-    return -1;
-}
-
 template <int SM, class STK, bool LOBJ = false>
 __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const RayC& rc, const RayF4& rq, double tmin,
-                                 float tmin32, int node, int& sp, const STK& stk, uint32_t smask, double& best,
-                                 double& bend, int& bp, float& best32 RS_ST_PARAMS) {
+                                 float tmin32, int node, int& sp, const STK& stk, double& best, double& bend,
+                                 int& bp, float& best32 RS_ST_PARAMS) {
 #ifdef RS_TRAV_STATS
 #define RS_ST_LEAF4() ++st_leaves
 #else
@@ -506,17 +475,16 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
         RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
 #undef RS_CS
-        // the cnt - 1 farther children are pushed (with their entries, stk_word); inside the LDS part
-        // all three writes are issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
-        const int w0 = stk_word(n0, e0, smask), w1 = stk_word(n1, e1, smask), w2 = stk_word(n2, e2, smask);
+        // the cnt - 1 farther children are pushed; inside the LDS part all three writes are
+        // issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
         if (!STK::kOvf || sp + 3 <= kStackMax) {
-            stk.lds[sp * kBlock] = w0;
-            stk.lds[(sp + 1) * kBlock] = w1;
-            stk.lds[(sp + 2) * kBlock] = w2;
+            stk.lds[sp * kBlock] = n0;
+            stk.lds[(sp + 1) * kBlock] = n1;
+            stk.lds[(sp + 2) * kBlock] = n2;
         } else {
-            if (cnt > 1) stk.put(sp, w0);
-            if (cnt > 2) stk.put(sp + 1, w1);
-            if (cnt > 3) stk.put(sp + 2, w2);
+            if (cnt > 1) stk.put(sp, n0);
+            if (cnt > 2) stk.put(sp + 1, n1);
+            if (cnt > 3) stk.put(sp + 2, n2);
         }
         sp += cnt - 1;
         next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
@@ -534,7 +502,10 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
         else break;
         RS_LEAF4(code);
     }
-    if (cnt == 0) next = stk_pop(stk, sp, smask, best32);  // with the range the leaves left
+    if (cnt == 0 && sp > 0) {
+        --sp;
+        next = stk.get(sp);
+    }
     return next;
 #undef RS_LEAF4
 #undef RS_ST_LEAF4
@@ -558,7 +529,7 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #define RS_LEAFQ_THR 48  // leaf pass at >= 48/64 of the working lanes with an entry queued
 template <int SM, class STK>
 __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, float tmin32, float best32, int node, int& sp,
-                                           const STK& stk, uint32_t smask, int* q, int& qt) {
+                                           const STK& stk, int* q, int& qt) {
     f4v NX, FX, NY, FY, NZ, FZ;
     i4v NC;
     load_node4(S, rq, node, NX, FX, NY, FY, NZ, FZ, NC);
@@ -590,20 +561,20 @@ __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, flo
                     (e2 > -__builtin_huge_valf()) + (e3 > -__builtin_huge_valf());
     int next;
     if (cnt == 0) {
-        next = stk_pop(stk, sp, smask, best32);
+        next = -1;
+        if (sp > 0) { --sp; next = stk.get(sp); }
     } else {
 #define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
         RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
 #undef RS_CS
-        const int w0 = stk_word(n0, e0, smask), w1 = stk_word(n1, e1, smask), w2 = stk_word(n2, e2, smask);
         if (!STK::kOvf || sp + 3 <= kStackMax) {
-            stk.lds[sp * kBlock] = w0;
-            stk.lds[(sp + 1) * kBlock] = w1;
-            stk.lds[(sp + 2) * kBlock] = w2;
+            stk.lds[sp * kBlock] = n0;
+            stk.lds[(sp + 1) * kBlock] = n1;
+            stk.lds[(sp + 2) * kBlock] = n2;
         } else {
-            if (cnt > 1) stk.put(sp, w0);
-            if (cnt > 2) stk.put(sp + 1, w1);
-            if (cnt > 3) stk.put(sp + 2, w2);
+            if (cnt > 1) stk.put(sp, n0);
+            if (cnt > 2) stk.put(sp + 1, n1);
+            if (cnt > 3) stk.put(sp + 2, n2);
         }
         sp += cnt - 1;
         next = cnt == 1 ? n0 : cnt == 2 ? n1 : cnt == 3 ? n2 : n3;
@@ -623,10 +594,8 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
     double best = RS_INF, bend = RS_INF;
     float best32 = __builtin_huge_valf();
     int bp = -1, node = S.root4, sp = 0, qh = 0, qt = 0;
-    const uint32_t smask = S.stk_mask;
 #ifdef RS_TRAV_STATS
     int st_nodes = 0, st_leaves = 0, st_witer = 0;
-    st_reset();
 #endif
     while (true) {
         const bool has_leaf = qt != qh;
@@ -652,7 +621,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
 #ifdef RS_TRAV_STATS
             ++st_nodes;
 #endif
-            node = bvh4_node_q<SM>(S, rq, tmin32, best32, node, sp, stk, smask, q, qt);
+            node = bvh4_node_q<SM>(S, rq, tmin32, best32, node, sp, stk, q, qt);
         }
     }
 #ifdef RS_TRAV_STATS
@@ -749,7 +718,6 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
     int sp = 0;
 #ifdef RS_TRAV_STATS
     int st_nodes = 0, st_leaves = 0, st_witer = 0;
-    st_reset();
 #define RS_ST_NODE() ++st_nodes
 #define RS_ST_LEAF() ++st_leaves
 #else
@@ -807,11 +775,10 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
     } else if (S.root4 >= 0 && !S.ref_order) {
         // 4-wide near-first (bvh4_step): nearest inner child next, the rest pushed far-to-near
         const RayF4 rq = make_rayf4(rf);
-        const uint32_t smask = S.stk_mask;
         node = S.root4;
         while (node >= 0) {
             RS_ST_NODE();
-            node = bvh4_step<SM, STK, LOBJ>(S, r, rc, rq, tmin, tmin32, node, sp, stk, smask, best, bend, bp, best32 RS_ST_PASS);
+            node = bvh4_step<SM, STK, LOBJ>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
         }
     } else if ((SM == kSmSpheres || SM == kSmFlat || SM == kSmGeneric) && !S.ref_order) {
         // binary near-first (monotone scenes without the 4-wide tree); the nest modes use the

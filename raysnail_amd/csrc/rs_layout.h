@@ -208,10 +208,6 @@ struct DScene {
     int32_t uv;              // 1: hit records carry (u, v) (some texture reads them: Image)
     int32_t has_media;       // 1: the scene has ConstantMedium objects (rays carry the medium key)
     int32_t stack_need;      // exact worst-case traversal stack depth of the tree in use (host-computed)
-    // 4-wide near-first stacks: a pushed node's word carries its entry distance in the bits above its
-    // index (the f32 entry's high bits: a lower bound), so a pop can drop a node the range has passed
-    // by. stk_mask = the index bits (2^k - 1 for 2^k >= nodes); all ones (no entry bits) above 2^24 nodes.
-    uint32_t stk_mask;
     int32_t moving;          // 1: some sphere has a nonzero speed (center_at needs the time)
     float bg_lo[4], bg_hi[4];
 };

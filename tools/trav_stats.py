@@ -27,7 +27,6 @@ for name in names:
           f"wave-max nodes {wmax/max(waves,1):.2f} live lanes/wave {lanes/max(waves,1):.1f} "
           f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f} "
           f"leaf passes/wave {witer/max(waves,1):.2f} leaf-pass lane use {leaves/max(64*witer,1):.3f}", flush=True)
-    print(f"  pops/ray {out[24]/max(rays,1):.2f}  pops a stored entry would cull {out[25]/max(out[24],1):.3f}", flush=True)
     hist = list(out[8:24])
     tot = max(1, sum(hist))
     print("  node steps per ray, 8-wide buckets (%):", " ".join(f"{8*b}:{100*h/tot:.1f}" for b, h in enumerate(hist)), flush=True)
