@@ -365,6 +365,19 @@ def test_streaming_pool_and_async_bit_identical(gpu, name):
             ds.render_device(cam.desc, sh, share.data_ptr(), s, stats=False)
         torch.cuda.synchronize()
         assert np.array_equal(share.cpu().numpy(), ref), frames
+        # the two settings on two streams at once: a slot is reused only after its previous frame
+        # (whatever stream it ran on), and each frame orders itself after its caller's stream
+        sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+        for o in outs:
+            o.fill_(-1.0)
+        sa.wait_stream(torch.cuda.current_stream())
+        sb.wait_stream(torch.cuda.current_stream())
+        for k in range(4):
+            ds.render_device(cam.desc, st if k % 2 == 0 else st2, outs[k % 2].data_ptr(),
+                             (sa if k % 2 == 0 else sb).cuda_stream, stats=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(outs[0].cpu().numpy(), ref), frames
+        assert np.array_equal(outs[1].cpu().numpy(), ref2), frames
     ds.set_frames_in_flight(2)
 
 
@@ -405,8 +418,8 @@ def test_queue_counter_reset_across_frames(gpu):
 def _emissive_csg_scene(w=80, h=60):
     """Composite prims whose records carry a DiffuseLight (an Intersection with the light on the
     CSG, a TfFacade of it) next to Lambertian CSG: the material-sorted wavefront must emit for them
-    (camera.rs:172-176, 250) although their shading class is the generic one, and Lambertian-only
-    CSG must get the Lambertian class (set_material_if_none, hit.rs:69-78)."""
+    (camera.rs:172-176, 250) from the generic class 4, which every composite prim gets -- Lambertian-only
+    CSG included (its records take the material through set_material_if_none, hit.rs:69-78)."""
     from raysnail_amd.api import (Box, CameraBuilder, DiffuseLight, Gradient, HittableList, Intersection,
                                   Lambertian, Sphere, TfFacade, Transform, TransformStack, World)
     from raysnail_amd.scenes import C32

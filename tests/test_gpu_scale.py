@@ -108,6 +108,16 @@ def test_virtual_devices_render_device(gpu):
     stats = ds.render_device(cam.desc, st, t.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert stats.samples == 64 * 40 * 4 and stats.kernel_launches > 0
     assert np.array_equal(t.cpu().numpy(), host)
+    # asynchronous (no stats): the second device's rows are ordered after the caller's stream by the
+    # frame's entry event and copied into the first device's buffer; two frames in flight on a side
+    # stream, the buffers reset on the caller's stream first
+    side = torch.cuda.Stream()
+    for k in range(3):
+        t.fill_(-1.0)
+        side.wait_stream(torch.cuda.current_stream())
+        assert ds.render_device(cam.desc, st, t.data_ptr(), side.cuda_stream, stats=False) is None
+        torch.cuda.current_stream().wait_stream(side)
+        assert np.array_equal(t.cpu().numpy(), host), k
 
 
 def test_host_only_commit_refuses_render(gpu):
