@@ -854,8 +854,8 @@ __device__ __forceinline__ bool leafish_hit(const DScene& S, int pi, const Ray& 
         if (P.kind == PK_XFORM) {
             const DXform X = S.xforms[P.idx];
             Ray rr = r;
-            rr.o = tf_inverse(S, X, P.aux, r.o, 1.0);
-            rr.d = tf_inverse(S, X, P.aux, r.d, 0.0);
+            rr.o = r.o; rr.d = r.d;
+            tf_inverse_ray(S, X, P.aux, rr.o, rr.d);
             if (!leafish_hit<L - 1>(S, X.child, rr, tmin, tmax, h)) return false;
             h.p = tf_forward(S, X, P.aux, h.p, 1.0);
             return true;
@@ -1356,7 +1356,10 @@ constexpr int kClsLight = 6;
 // camera-ray extend 144 -> 128 VGPRs: bench frame 7.86 -> 7.63 ms; nest-0 129 -> 128: example.sdl
 // 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 2 (unbounded, the camera part took
 // 2 AGPRs beyond 256 VGPRs: one wave per SIMD; 3 waves spilled 288 B)
-constexpr int ext_min_waves(int sm) { return sm == kSmNest2 ? 2 : 4; }
+#ifndef RS_N2W
+#define RS_N2W 3
+#endif
+constexpr int ext_min_waves(int sm) { return sm == kSmNest2 ? RS_N2W : 4; }
 
 // The scene's LDS image (DScene::limg, nest modes): the block copies it into its dynamic LDS and
 // reads the tree and the object tables through a DScene copy whose table pointers point there.
@@ -1465,8 +1468,8 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const 
                             Obj<0, 0>::hit_t(S, bp, r, 0.0001, bend, ht);
                             h.p = ht.p;
                             mi = S.prims[bp].mat;
-                        } else {
-                            finish_hit<SM>(S, bp, r, 0.0001, bend, h);
+                        } else {  // a TfFacade chain over a leaf (light-class prims are leafish)
+                            finish_hit<SM, true>(S, bp, r, 0.0001, bend, h);
                             mi = h.mat;
                         }
                     }
@@ -1575,8 +1578,11 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // per-class launch tails (the small classes' queues take 5-50 us each however short they are).
 // G4: the scene has class-4 prims (the generic material switch, composite objects), compiled in only
 // then (it sets the kernel's register count). LOBJ: the scene's tables from its LDS image (lds_scene).
+#ifndef RS_N2S
+#define RS_N2S 1
+#endif
 template <int SM, bool G4, bool LOBJ>
-__global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4) ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
+__global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4) ? RS_N2S : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
