@@ -1579,7 +1579,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // G4: the scene has class-4 prims (the generic material switch, composite objects), compiled in only
 // then (it sets the kernel's register count). LOBJ: the scene's tables from its LDS image (lds_scene).
 #ifndef RS_N2S
-#define RS_N2S 1
+#define RS_N2S 3
 #endif
 template <int SM, bool G4, bool LOBJ>
 __global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4) ? RS_N2S : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
