@@ -1677,8 +1677,17 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      ++ki;
                      ++path_launches;
                  };
+                 // nest-0: an iteration with only carried paths (or only camera samples) runs the
+                 // kernel compiled for that part alone (example.sdl 8.95 -> 8.41 ms); the spheres mode
+                 // keeps the merged kernel (its parts measured 2.8 % slower on the bench frame:
+                 // profiles/r4/ab/part_pick)
+                 const bool pick = sm != kSmSpheres;
                  if (split) {
                      extend(kExtCarried, window[l]);
+                     extend(kExtCamera, n_new);
+                 } else if (pick && n_new == 0) {
+                     extend(kExtCarried, window[l]);
+                 } else if (pick && window[l] == 0) {
                      extend(kExtCamera, n_new);
                  } else {
                      extend(kExtAll, window[l] + n_new);
