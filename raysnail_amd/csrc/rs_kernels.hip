@@ -1354,12 +1354,10 @@ constexpr int kClsLight = 6;
 
 // waves/SIMD the extend is bounded to: spheres and nest-0 scenes 4 (128 VGPRs; the spheres-mode
 // camera-ray extend 144 -> 128 VGPRs: bench frame 7.86 -> 7.63 ms; nest-0 129 -> 128: example.sdl
-// 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 2 (unbounded, the camera part took
-// 2 AGPRs beyond 256 VGPRs: one wave per SIMD; 3 waves spilled 288 B)
-#ifndef RS_N2W
-#define RS_N2W 3
-#endif
-constexpr int ext_min_waves(int sm) { return sm == kSmNest2 ? RS_N2W : 4; }
+// 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 with the LDS image 3 (168 VGPRs, 184 B
+// of scratch: 4 % faster than 2 waves, 4 waves 12 % slower; profiles/r4/ab/nest2_registers), nest-2
+// with its tables in global memory 2 (its loads are L1 / L2 round trips that the spills would join)
+constexpr int ext_min_waves(int sm, bool lobj = false) { return sm == kSmNest2 ? (lobj ? 3 : 2) : 4; }
 
 // The scene's LDS image (DScene::limg, nest modes): the block copies it into its dynamic LDS and
 // reads the tree and the object tables through a DScene copy whose table pointers point there.
@@ -1398,7 +1396,7 @@ __device__ __forceinline__ void lds_scene(const DScene* __restrict__ Sp, DScene&
 // against two waves for each part)
 // LOBJ: the scene's tables from its LDS image (lds_scene; the launch passes limg_bytes of dynamic LDS)
 template <int SM, bool OVF, int PART, bool LOBJ>
-__global__ __launch_bounds__(kBlock, ext_min_waves(SM)) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W,
+__global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W,
                                                                           uint32_t* const* __restrict__ queues, uint32_t it,
                                                                           double* __restrict__ rad, DCamera C, PathParams P,
                                                                           InjParams I) {
@@ -1578,11 +1576,10 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // per-class launch tails (the small classes' queues take 5-50 us each however short they are).
 // G4: the scene has class-4 prims (the generic material switch, composite objects), compiled in only
 // then (it sets the kernel's register count). LOBJ: the scene's tables from its LDS image (lds_scene).
-#ifndef RS_N2S
-#define RS_N2S 3
-#endif
+// Waves: 3; nest-2 with class 4 and the tables in global memory 1 (bounded to 3 it spilled and lost
+// 21 % on C4 in round 3; with the LDS image 3 waves measured 5 % faster than 2: nest2_registers)
 template <int SM, bool G4, bool LOBJ>
-__global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4) ? RS_N2S : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
+__global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
