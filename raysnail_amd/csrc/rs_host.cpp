@@ -219,7 +219,7 @@ struct Replica {
     Slot slots[kMaxSlots];
     uint32_t next_slot = 0;
     int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
-    int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond kStackMax)
+    int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond the LDS part)
     DScene* d_ds = nullptr;                 // ds in device memory (what the kernels read)
     DScene uploaded{};                      // the copy last written to d_ds
 
@@ -746,7 +746,7 @@ void build_limg(rs_scene* s) {
     if (s->scene_mode != kSmNest0 && s->scene_mode != kSmNest2) return;
     // the image's kernels walk the in-order 4-wide tree with their leaf list in the LDS stack's top
     // kLeafBatch entries (rs_kernels.hip traverse_deferred)
-    if (d.root4 < 0 || !d.ref_order || s->stack_need + (int)kLeafBatch > kStackMax) return;
+    if (d.root4 < 0 || !d.ref_order || s->stack_need + (int)kLeafBatch > stack_lds(s->scene_mode)) return;
     const uint32_t cap = kLimgMax;
 #ifdef RS_DEV_KNOBS
     if (std::getenv("RS_NO_LIMG")) return;  // the tables in global memory, for comparison
@@ -1299,7 +1299,7 @@ void ensure(Q& owner, T*& p, size_t& cap, size_t n) {
 // Traversal-stack overflow for launches of at most `threads` grid threads: (stack_need - kStackMax)
 // entries per thread (DScene::stk_ovf). Nothing is allocated when the tree fits the LDS stack.
 void ensure_stack_overflow(const rs_scene* s, Replica& R, uint64_t threads) {
-    const int extra = s->stack_need - kStackMax;
+    const int extra = s->stack_need - kStackMin;  // rows for the smallest LDS part (rs_internal.h stack_lds)
     if (extra <= 0) { R.ds.stk_ovf = nullptr; return; }
     ensure(R, R.d_ovf, R.ovf_cap, (size_t)extra * threads);
     R.ds.stk_ovf = R.d_ovf;
@@ -1531,7 +1531,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     if (n_rows == 0) return;
     P.empty = false;
     // one frame at a time for trees whose traversal stack spills to the replica's shared HBM overflow
-    const bool ext_spill = s->stack_need > kStackMax;
+    const bool ext_spill = s->stack_need > stack_lds(s->scene_mode);
     const uint32_t n_slots = ext_spill ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
     Slot& L = R.slots[R.next_slot % n_slots];
     R.next_slot = (R.next_slot + 1) % n_slots;
@@ -1955,7 +1955,7 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
             HIP_OK(hipStreamWaitEvent(R.stream, entry, 0));
             // this frame's copies of the mask and the frame live in R's next slot (the slot render_enqueue
             // picks): its previous frame must be done with them
-            const uint32_t n_slots = s->stack_need > kStackMax ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            const uint32_t n_slots = s->stack_need > stack_lds(s->scene_mode) ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
             Slot& L = R.slots[R.next_slot % n_slots];
             if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
             ensure(L, L.d_out, L.out_cap, npx * 4);
@@ -2018,7 +2018,7 @@ void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
             rows[k] = replica_rows(cam, st, k, n);
             if (rows[k].count() == 0) continue;
             DeviceGuard g(R.device);
-            const uint32_t n_slots = s->stack_need > kStackMax ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            const uint32_t n_slots = s->stack_need > stack_lds(s->scene_mode) ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
             Slot& L = R.slots[R.next_slot % n_slots];
             slot[k] = &L;
             if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
@@ -2102,7 +2102,7 @@ void render_frame_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
             bs.row_end = (uint32_t)std::min<uint64_t>(re, (uint64_t)bs.row_begin + (uint64_t)per * step);
             bs.row_step = step;
             rows[b] = replica_rows(cam, &bs, 0, 1);
-            const uint32_t n_slots = s->stack_need > kStackMax ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            const uint32_t n_slots = s->stack_need > stack_lds(s->scene_mode) ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
             Slot& L = R.slots[R.next_slot % n_slots];
             if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
             ensure(L, L.d_out, L.out_cap, npx * 4);
@@ -2429,7 +2429,7 @@ int rs_scene_get_info(const rs_scene* s, rs_scene_info* out) {
         out->scene_mode = s->scene_mode;
         out->tree_depth = s->tree_depth;
         out->stack_need = s->stack_need;
-        out->stack_lds = kStackMax;
+        out->stack_lds = stack_lds(s->scene_mode);
         out->n_nodes = s->n_nodes;
         out->n_objects = s->objs.size();
         out->n_world = s->world.size();

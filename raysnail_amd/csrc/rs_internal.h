@@ -10,6 +10,9 @@ constexpr int kBlock = 256;      // 4 waves of 64
 // per-thread BVH stack entries held in LDS (24 KiB/block -> 6 blocks/CU); deeper entries spill to
 // DScene::stk_ovf, which the host sizes from the tree's exact worst-case stack depth
 constexpr int kStackMax = 24;
+// the smallest LDS part of any path kernel (stack_lds below): the overflow array is sized for it, so
+// every kernel that walks a scene fits it
+constexpr int kStackMin = 16;
 // leaves listed per walk by the deferred reference-order traversal (LDS-image scenes), in the top
 // kLeafBatch entries of the thread's LDS stack column
 constexpr uint32_t kLeafBatch = 8;
@@ -30,6 +33,12 @@ constexpr int rich_of(int sm) { return sm == kSmGeneric ? 1 : 0; }
 // the streaming (material-sorted) wavefront serves these modes; flat (mesh) and generic scenes run
 // the bounce-synchronous unsorted wavefront
 constexpr bool streaming_mode(int sm) { return sm == kSmSpheres || sm == kSmNest0 || sm == kSmNest2; }
+// LDS stack entries per thread of the path kernels (k_wf_extend, k_wfs_extend) by scene mode: 16 for
+// meshes and nested objects, 24 elsewhere. A 32 KiB block (24 entries + the mesh extend's 8-entry leaf
+// FIFO) kept only 4 of the flat extend's 5 blocks per CU resident; at 16 entries the C5 mesh frame is
+// 10 % faster although more of its deep entries spill to HBM, C4 2.5 % and example.sdl 1.6 %; the
+// rich mode (X2) lost 4 % and the spheres mode is unchanged (profiles/r4/ab/lds_stack).
+constexpr int stack_lds(int sm) { return (sm == kSmFlat || sm == kSmNest0 || sm == kSmNest2) ? kStackMin : kStackMax; }
 
 // A committed scene for a launch: the host copy (launch decisions) and the same struct in device
 // memory, which the kernels read through a pointer (a by-value kernel argument that device functions

@@ -377,25 +377,28 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, 
 // thread's grid index, so the common path keeps no extra registers live.
 // OVF = false: the host guarantees stack_need + 3 <= kStackMax (no HBM part; the bvh4 push's three
 // unconditional writes stay inside the LDS column), so push / pop are plain LDS accesses.
-template <bool OVF>
+// N: the entries of the LDS part (stack_lds); the overflow rows start at entry N (the host sizes
+// them for the smallest N, kStackMin)
+template <bool OVF, int N = kStackMax>
 struct StkT {
     static constexpr bool kOvf = OVF;
+    static constexpr int kN = N;
     int* lds;          // this thread's column of the block's LDS stack
     int* ovf_base;     // DScene::stk_ovf (uniform)
     __device__ __forceinline__ int* ovf(int i) const {
-        return ovf_base + ((size_t)(i - kStackMax) * gridDim.x * kBlock + (size_t)blockIdx.x * kBlock + threadIdx.x);
+        return ovf_base + ((size_t)(i - N) * gridDim.x * kBlock + (size_t)blockIdx.x * kBlock + threadIdx.x);
     }
     __device__ __forceinline__ void put(int i, int v) const {
-        if (!OVF || i < kStackMax) lds[i * kBlock] = v;
+        if (!OVF || i < N) lds[i * kBlock] = v;
         else *ovf(i) = v;
     }
-    __device__ __forceinline__ int get(int i) const { return (!OVF || i < kStackMax) ? lds[i * kBlock] : *ovf(i); }
+    __device__ __forceinline__ int get(int i) const { return (!OVF || i < N) ? lds[i * kBlock] : *ovf(i); }
 };
 using Stk = StkT<true>;
-// this thread's stack (stk_all = the block's LDS array)
-template <bool OVF = true>
-__device__ __forceinline__ StkT<OVF> make_stk(const DScene& S, int* stk_all) {
-    StkT<OVF> s;
+// this thread's stack (stk_all = the block's LDS array of N x kBlock entries)
+template <bool OVF = true, int N = kStackMax>
+__device__ __forceinline__ StkT<OVF, N> make_stk(const DScene& S, int* stk_all) {
+    StkT<OVF, N> s;
     s.lds = stk_all + threadIdx.x;
     s.ovf_base = S.stk_ovf;
     return s;
@@ -477,7 +480,7 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 #undef RS_CS
         // the cnt - 1 farther children are pushed; inside the LDS part all three writes are
         // issued (the ones above sp + cnt - 1 are dead), near its end only the live ones
-        if (!STK::kOvf || sp + 3 <= kStackMax) {
+        if (!STK::kOvf || sp + 3 <= STK::kN) {
             stk.lds[sp * kBlock] = n0;
             stk.lds[(sp + 1) * kBlock] = n1;
             stk.lds[(sp + 2) * kBlock] = n2;
@@ -567,7 +570,7 @@ __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, flo
 #define RS_CS(EA, NA, EB, NB) if (EB > EA) { const float te = EA; EA = EB; EB = te; const int tn = NA; NA = NB; NB = tn; }
         RS_CS(e0, n0, e1, n1) RS_CS(e2, n2, e3, n3) RS_CS(e0, n0, e2, n2) RS_CS(e1, n1, e3, n3) RS_CS(e1, n1, e2, n2)
 #undef RS_CS
-        if (!STK::kOvf || sp + 3 <= kStackMax) {
+        if (!STK::kOvf || sp + 3 <= STK::kN) {
             stk.lds[sp * kBlock] = n0;
             stk.lds[(sp + 1) * kBlock] = n1;
             stk.lds[(sp + 2) * kBlock] = n2;
@@ -646,7 +649,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
 template <int SM, class STK>
 __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     constexpr uint32_t K = kLeafBatch;
-    int* const q = stk.lds + (kStackMax - (int)K) * kBlock;  // this thread's list slots
+    int* const q = stk.lds + (STK::kN - (int)K) * kBlock;  // this thread's list slots
     const RayC rc = ray_consts(r);
     const float tmin32 = -round_up_f(-tmin);
     double best = RS_INF, bend = RS_INF;
@@ -1274,8 +1277,8 @@ constexpr int kWfExtFlatWaves = 5;
 template <int SM>
 __global__ __launch_bounds__(kBlock, SM == kSmFlat ? kWfExtFlatWaves : 1) void k_wf_extend(const DScene* __restrict__ Sp, WfState W, uint32_t bounce) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
-    __shared__ int stk_all[kStackMax * kBlock];
-    const Stk stk = make_stk(S, stk_all);
+    __shared__ int stk_all[stack_lds(SM) * kBlock];
+    const StkT<true, stack_lds(SM)> stk = make_stk<true, stack_lds(SM)>(S, stk_all);
     __shared__ int leafq[SM == kSmFlat ? RS_LEAFQ * kBlock : 1];
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
@@ -1403,8 +1406,8 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
     DScene Sv;
     if constexpr (LOBJ) lds_scene(Sp, Sv, false);  // filled in the first pass of the loop below
     const DScene& S = LOBJ ? Sv : *Sp;  // otherwise the scene in device memory (no by-value copy in scratch)
-    __shared__ int stk_all[kStackMax * kBlock];
-    const StkT<OVF> stk = make_stk<OVF>(S, stk_all);
+    __shared__ int stk_all[stack_lds(SM) * kBlock];
+    const StkT<OVF, stack_lds(SM)> stk = make_stk<OVF, stack_lds(SM)>(S, stk_all);
     uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
     const uint32_t nf = cnt[cix(kCntFront)];
     const uint32_t n_old = PART == kExtCamera ? 0u : nf + cnt[cix(kCntBack)];
@@ -1443,7 +1446,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
             if (base == blockIdx.x * kBlock) lds_fill(S);
         if (live) {
             double bend = RS_INF;
-            const int bp = traverse<SM, StkT<OVF>, LOBJ>(S, r, 0.0001, bend, stk);
+            const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ>(S, r, 0.0001, bend, stk);
             V3 add;
             bool done = true;
             if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
@@ -1846,7 +1849,7 @@ hipError_t wf_occupancy_sm(int* e, int* sh) {
 
 // the LDS-only traversal stack (StkT<false>) where the tree allows it; spheres mode only (the other
 // modes keep one instantiation each: compile time)
-[[maybe_unused]] static inline bool lds_only_stack(const SceneRef& s) { return s.host->stack_need + 3 <= kStackMax; }
+[[maybe_unused]] static inline bool lds_only_stack(const SceneRef& s, int sm) { return s.host->stack_need + 3 <= stack_lds(sm); }
 
 template <int SMC>
 hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w, uint32_t* const* queues,
@@ -1868,7 +1871,7 @@ hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& 
         else if (part == kExtCamera) { if (shm) RS_EXT_LAUNCH_L(true, kExtCamera, true, shm); else RS_EXT_LAUNCH(true, kExtCamera); }
         else { if (shm) RS_EXT_LAUNCH_L(true, kExtCarried, true, shm); else RS_EXT_LAUNCH(true, kExtCarried); }
     } else if constexpr (SMC == kSmSpheres) {
-        const bool lds = lds_only_stack(s);
+        const bool lds = lds_only_stack(s, SMC);
         if (part == kExtAll) { if (lds) RS_EXT_LAUNCH(false, kExtAll); else RS_EXT_LAUNCH(true, kExtAll); }
         else if (part == kExtCamera) { if (lds) RS_EXT_LAUNCH(false, kExtCamera); else RS_EXT_LAUNCH(true, kExtCamera); }
         else { if (lds) RS_EXT_LAUNCH(false, kExtCarried); else RS_EXT_LAUNCH(true, kExtCarried); }

@@ -15,7 +15,7 @@ from raysnail_amd import _abi as A
 from raysnail_amd import api, scenes
 
 pytestmark = pytest.mark.gpu
-KSTACK_LDS = 24
+KSTACK_LDS = 16  # the flat mode's LDS stack entries (rs_internal.h stack_lds)
 
 
 def _oracle(world):
