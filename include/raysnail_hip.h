@@ -290,7 +290,9 @@ int rs_scene_set_frames_in_flight(rs_scene* s, uint32_t frames);
 /* workspace sizes (0 = keep): camera samples per radiance batch buffer (default 32 Mi, whole sample
  * planes are used) and paths per path set (default 64 Mi: the bound of the streaming wavefront's pool
  * -- camera samples injected per iteration times the iterations a path can span -- and the chunk of
- * the bounce-synchronous wavefront). Scheduling only: frames are bitwise the same for any value. */
+ * the bounce-synchronous wavefront). pool_paths is a soft bound: an iteration injects at least 256
+ * samples (one block), so a pool below 256 x depth paths is raised to that for the frame.
+ * Scheduling only: frames are bitwise the same for any value. */
 int rs_scene_set_workspace(rs_scene* s, uint64_t max_batch_items, uint64_t pool_paths);
 
 /* ---- render ---- */
@@ -304,7 +306,8 @@ int rs_render(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* 
  * band is complete, cb(user, y, row, W) is called for each of its rows y (row = out_rgba's row y,
  * already written), from the calling thread, in band order, while the later bands are traced; then
  * cb(user, H, NULL, 0). Rows off the lattice are neither written nor reported. The frame is bitwise
- * the rs_render frame. With stats, bands are rendered one at a time (timed). */
+ * the rs_render frame. Stats carry the counts (samples, segments, kernel_bytes, tree_arity) and the call's
+ * wall time `ms`; the bands stay in flight together, so no per-kernel device times are taken (0). */
 typedef void (*rs_row_callback)(void* user, uint32_t y, const float* row_rgba, uint32_t width);
 int rs_render_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, const uint8_t* mask,
                    float* out_rgba, uint32_t bands, rs_row_callback cb, void* user, rs_render_stats* stats);

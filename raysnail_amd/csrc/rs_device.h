@@ -1101,6 +1101,7 @@ __device__ __forceinline__ Ray camera_ray(const DCamera& c, double u, double v, 
     r.o = o;
     r.d = unit(dir);
     r.time = c.shutter * rng.gen();
+    r.key = 0;
     return r;
 }
 

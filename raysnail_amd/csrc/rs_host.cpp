@@ -182,6 +182,10 @@ struct Slot {
     size_t counts_clean = 0;  // leading entries of d_counts known to be zero (reset by the last frame's accumulate)
     hipStream_t acc_stream = nullptr;         // streaming wavefront: the batches' accumulates
     std::vector<hipEvent_t> bev;              // per batch: its paths done, its accumulate done
+    // streaming wavefront: the frame's CamConsts + every iteration's InjParams (device copy, pinned staging,
+    // the event of the last upload: the staging is rewritten only once that copy has run)
+    void* d_fc = nullptr; void* h_fc = nullptr; size_t fc_cap = 0;
+    hipEvent_t fc_ev = nullptr; bool fc_rec = false;
 
     // wait until nothing in flight uses this slot's buffers
     void quiesce() {
@@ -189,14 +193,18 @@ struct Slot {
             if (lane[l]) HIP_OK(hipStreamSynchronize(lane[l]));
         if (acc_stream) HIP_OK(hipStreamSynchronize(acc_stream));
         if (free_rec) HIP_OK(hipEventSynchronize(free_ev));
+        if (fc_rec) HIP_OK(hipEventSynchronize(fc_ev));
     }
     void release() {
         for (uint32_t l = 0; l < kMaxLanes; ++l)
             if (lane[l]) (void)hipStreamSynchronize(lane[l]);
         if (acc_stream) (void)hipStreamSynchronize(acc_stream);
         if (free_rec) (void)hipEventSynchronize(free_ev);
-        for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts})
+        if (fc_rec) (void)hipEventSynchronize(fc_ev);
+        for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts, d_fc})
             if (p) (void)hipFree(p);
+        if (h_fc) (void)hipHostFree(h_fc);
+        if (fc_ev) (void)hipEventDestroy(fc_ev);
         for (uint32_t l = 0; l < kMaxLanes; ++l) {
             if (lane[l]) (void)hipStreamDestroy(lane[l]);
             if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
@@ -274,6 +282,8 @@ struct rs_scene {
     uint32_t stream_lanes = 1;                    // lanes of the streaming wavefront (rs_scene_set_lanes)
     uint32_t frames_in_flight = 2;                // frame slots per replica (rs_scene_set_frames_in_flight)
     bool ext_split = false;                       // streaming extend in two launches per iteration in every mode (dev A/B)
+    bool split_runs = false;                      // dev: carried front run / the rest in separate extend launches
+    bool dump_iters = false;                      // dev: per-iteration queue counts to stderr (timed frames)
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
     int tree_depth = 0;                     // levels of the tree in use
     int tree_arity = 0;                     // 4: 4-wide tree, 2: binary tree, 0: empty world
@@ -953,9 +963,6 @@ void build(rs_scene* s) {
 #ifdef RS_DEV_KNOBS
     if (const char* ev = std::getenv("RS_SAH_DEPTH")) B.sah_depth = std::max(0, std::atoi(ev));
     if (const char* ev = std::getenv("RS_SAH_SWEEP")) B.kSweepMax = (size_t)std::max(2LL, std::atoll(ev));
-    const bool no_bvh4 = std::getenv("RS_NO_BVH4") != nullptr;  // the binary trees, for comparison
-#else
-    const bool no_bvh4 = false;
 #endif
     int32_t root = -1;
     if (!items.empty()) {
@@ -1072,7 +1079,7 @@ void build(rs_scene* s) {
     if (root >= 0)
         s->stack_need = s->ref_order ? stack_need_ref(B.nodes, root)
                                      : std::max(stack_need_ref(B.nodes, root), stack_need2(B.nodes, root));
-    if (!s->ref_order && root >= 0 && !no_bvh4) {
+    if (!s->ref_order && root >= 0) {
         std::vector<HNode4> n4;
         int depth4 = 0;
         const int32_t r4 = collapseW<4>(B.nodes, root, n4, 0, depth4);
@@ -1091,7 +1098,7 @@ void build(rs_scene* s) {
     }
     // reference-order scenes on the in-order 4-wide tree (collapse4_inorder), nest-0 / nest-2 modes (the
     // generic mode measured 3 % slower on it: X2)
-    if (s->ref_order && (s->scene_mode == kSmNest0 || s->scene_mode == kSmNest2) && root >= 0 && !no_bvh4) {
+    if (s->ref_order && (s->scene_mode == kSmNest0 || s->scene_mode == kSmNest2) && root >= 0) {
         std::vector<HNode4> n4;
         int depth4 = 0;
         const int32_t r4 = collapse4_inorder(B.nodes, root, n4, 0, depth4);
@@ -1485,7 +1492,8 @@ struct Pending {
     hipStream_t stream = nullptr;   // the stream the frame ends on (the caller's, or the replica's own)
     bool empty = true;
     int kind = 0;                   // 0 megakernel, 1 bounce-synchronous wavefront, 2 streaming wavefront
-    bool timed = false;
+    bool timed = false;             // per-kernel events; the frame runs alone
+    bool counted = false;           // the queue counters are kept for render_finish (statistics)
     uint32_t n_pix = 0, N = 0, depth = 0, n_batches = 0, path_launches = 0;
     uint64_t n_chunks_total = 0;
     std::vector<LaneSched> lanes;               // streaming: the lanes' schedules
@@ -1499,6 +1507,14 @@ struct Pending {
         for (auto& e : kev) (void)hipEventDestroy(e);
     }
 };
+
+// Frame slots a replica cycles through (render_enqueue takes slot next_slot % frame_slots): one for trees
+// whose traversal stack spills to the replica's shared HBM overflow array, else frames_in_flight. Callers
+// that keep several frames (bands) in flight must not exceed it: two frames in one slot share its counters.
+uint32_t frame_slots(const rs_scene* s) {
+    if (s->stack_need > stack_lds(s->scene_mode)) return 1u;
+    return std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+}
 
 void validate_render(const rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st) {
     if (!cam || !st) throw Error(RS_E_INVALID, "null argument");
@@ -1518,21 +1534,43 @@ hipStream_t lane_stream(Slot& L, uint32_t l) {
     return L.lane[l];
 }
 
+// The camera samples lane ln injects at iteration t (InjParams): the frame's enqueue and the shading's
+// regeneration of camera samples (CamConsts upload) use the same values.
+InjParams inj_params(const FrameSched& f, const LaneSched& ln, uint64_t t, uint64_t ring_items) {
+    InjParams I{};
+    I.n_new = ln.n_new(t);
+    I.ring = ring_items;
+    if (I.n_new) {
+        const uint64_t j0 = t * ln.Q, m = j0 / f.B;
+        const uint32_t k = ln.batch[m];
+        I.jb0 = (uint32_t)(j0 - m * f.B);
+        I.nb0 = (uint32_t)ln.nb(m);
+        I.nb1 = m + 1 < ln.batch.size() ? (uint32_t)ln.nb(m + 1) : 0u;
+        I.g0 = (uint64_t)k * f.B;
+        I.g1 = m + 1 < ln.batch.size() ? (uint64_t)ln.batch[m + 1] * f.B : 0u;
+        I.rad0 = (uint32_t)((k % f.ring) * f.B);
+        I.rad1 = m + 1 < ln.batch.size() ? (uint32_t)((ln.batch[m + 1] % f.ring) * f.B) : 0u;
+    }
+    return I;
+}
+
 // Enqueue the rows `rows` of the frame on replica R (its device must be current): camera samples ->
 // wavefront (streaming or bounce-synchronous) or megakernel -> ordered accumulation -> into_color into
 // d_out (W*H RGBA on R's device), the last step on `S`, the stream the frame ends on. The path work
 // runs on one of R's frame slots. Nothing here waits for the device.
 void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, const rs_render_settings* st,
-                    RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t S, Pending& P, bool timed) {
+                    RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t S, Pending& P, bool timed,
+                    bool counted) {
     P.R = &R;
     P.stream = S;
     P.timed = timed;
+    P.counted = counted = counted || timed;
     const uint32_t n_rows = rows.count();
     if (n_rows == 0) return;
     P.empty = false;
     // one frame at a time for trees whose traversal stack spills to the replica's shared HBM overflow
     const bool ext_spill = s->stack_need > stack_lds(s->scene_mode);
-    const uint32_t n_slots = ext_spill ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+    const uint32_t n_slots = frame_slots(s);
     Slot& L = R.slots[R.next_slot % n_slots];
     R.next_slot = (R.next_slot + 1) % n_slots;
     P.L = &L;
@@ -1615,6 +1653,37 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         for (uint32_t l = 1; l < f.lanes; ++l) ls[l] = lane_stream(L, l);
         if (!L.acc_stream) HIP_OK(hipStreamCreateWithFlags(&L.acc_stream, hipStreamNonBlocking));
         if (!L.fork_ev) HIP_OK(hipEventCreateWithFlags(&L.fork_ev, hipEventDisableTiming));
+        const uint64_t ring_items = (uint64_t)f.ring * f.B;
+        // the frame's CamConsts and every iteration's InjParams for the shading (one upload on L0, before the fork)
+        std::vector<size_t> it_off(f.lanes, 0);
+        size_t n_it = 0;
+        for (uint32_t l = 0; l < f.lanes; ++l) { it_off[l] = n_it; n_it += f.lane[l].T; }
+        const size_t fc_head = (sizeof(CamConsts) + 63) & ~(size_t)63;
+        const size_t fc_bytes = fc_head + n_it * sizeof(InjParams);
+        if (fc_bytes > L.fc_cap) {
+            L.quiesce();
+            if (L.d_fc) HIP_OK(hipFree(L.d_fc));
+            if (L.h_fc) HIP_OK(hipHostFree(L.h_fc));
+            L.d_fc = L.h_fc = nullptr;
+            L.fc_cap = 0;
+            HIP_OK(hipMalloc(&L.d_fc, fc_bytes));
+            HIP_OK(hipHostMalloc(&L.h_fc, fc_bytes, hipHostMallocDefault));
+            L.fc_cap = fc_bytes;
+        }
+        if (!L.fc_ev) HIP_OK(hipEventCreateWithFlags(&L.fc_ev, hipEventDisableTiming));
+        if (L.fc_rec) HIP_OK(hipEventSynchronize(L.fc_ev));  // the staging's previous upload has run
+        {
+            CamConsts cc{dc, pp};
+            std::memcpy(L.h_fc, &cc, sizeof(cc));
+            InjParams* hi = (InjParams*)((char*)L.h_fc + fc_head);
+            for (uint32_t l = 0; l < f.lanes; ++l)
+                for (uint64_t t = 0; t < f.lane[l].T; ++t) hi[it_off[l] + t] = inj_params(f, f.lane[l], t, ring_items);
+        }
+        HIP_OK(hipMemcpyAsync(L.d_fc, L.h_fc, fc_bytes, hipMemcpyHostToDevice, L0));
+        HIP_OK(hipEventRecord(L.fc_ev, L0));
+        L.fc_rec = true;
+        const CamConsts* d_cc = (const CamConsts*)L.d_fc;
+        const InjParams* d_inj = (const InjParams*)((const char*)L.d_fc + fc_head);
         HIP_OK(hipEventRecord(L.fork_ev, L0));
         for (uint32_t l = 1; l < f.lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], L.fork_ev, 0));
         HIP_OK(hipStreamWaitEvent(L.acc_stream, L.fork_ev, 0));
@@ -1628,7 +1697,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         auto acc_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k + 1]; };
         const bool split = ext_split(sm) || s->ext_split;
         size_t n_ext = 0;
-        for (const LaneSched& ln : f.lane) n_ext += ln.T * (split ? 2 : 1);
+        for (const LaneSched& ln : f.lane) n_ext += ln.T * (split || s->split_runs ? 2 : 1);
         P.kev.assign(timed ? 2 * n_ext : 0, nullptr);
         for (auto& e : P.kev) e = new_ev();
         P.ev.assign(timed ? 2 : 0, nullptr);  // path_ms: the frame's iterations
@@ -1640,7 +1709,6 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         std::vector<uint64_t> window(f.lanes, 0), m_done(f.lanes, 0);
         std::vector<std::vector<uint32_t>> inj(f.lanes);
         for (uint32_t l = 0; l < f.lanes; ++l) inj[l].assign(f.lane[l].T, 0u);
-        const uint64_t ring_items = (uint64_t)f.ring * f.B;
         walk(f,
              [&](uint32_t l, uint64_t t) {
                  const LaneSched& ln = f.lane[l];
@@ -1650,19 +1718,9 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  uint32_t** qd = L.d_qptrs[l];
                  const uint32_t n_new = ln.n_new(t);
                  inj[l][t] = n_new;
-                 InjParams I{};
-                 I.n_new = n_new;
-                 I.ring = ring_items;
+                 InjParams I = inj_params(f, ln, t, ring_items);
                  if (n_new) {
-                     const uint64_t j0 = t * ln.Q, m = j0 / f.B;
-                     const uint32_t k = ln.batch[m];
-                     I.jb0 = (uint32_t)(j0 - m * f.B);
-                     I.nb0 = (uint32_t)ln.nb(m);
-                     I.nb1 = m + 1 < ln.batch.size() ? (uint32_t)ln.nb(m + 1) : 0u;
-                     I.g0 = (uint64_t)k * f.B;
-                     I.g1 = m + 1 < ln.batch.size() ? (uint64_t)ln.batch[m + 1] * f.B : 0u;
-                     I.rad0 = (uint32_t)((k % f.ring) * f.B);
-                     I.rad1 = m + 1 < ln.batch.size() ? (uint32_t)((ln.batch[m + 1] % f.ring) * f.B) : 0u;
+                     const uint64_t m = t * ln.Q / f.B;
                      // a batch taking over a ring buffer: after the batch `ring` earlier was accumulated
                      for (uint64_t mm = m; mm <= m + 1 && mm < ln.batch.size(); ++mm) {
                          const uint32_t kk = ln.batch[mm];
@@ -1682,6 +1740,15 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  // keeps the merged kernel (its parts measured 2.8 % slower on the bench frame:
                  // profiles/r4/ab/part_pick)
                  const bool pick = sm != kSmSpheres;
+#ifdef RS_DEV_KNOBS
+                 if (s->split_runs && n_new == 0 && !split && window[l]) {  // dev: the front run and the rest timed apart
+                     I.run = 1;
+                     extend(pick ? kExtCarried : kExtAll, window[l]);
+                     I.run = 2;
+                     extend(pick ? kExtCarried : kExtAll, window[l]);
+                     I.run = 0;
+                 } else
+#endif
                  if (split) {
                      extend(kExtCarried, window[l]);
                      extend(kExtCamera, n_new);
@@ -1694,7 +1761,8 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  }
                  if (D > 0) {
                      const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + n_new + kBlock - 1) / kBlock);
-                     HIP_OK(launch_wfs_shade_all(ds, WS, qd, s->class_mask, (uint32_t)t, D, ring_items, L.d_rad, b, sm, cs));
+                     HIP_OK(launch_wfs_shade_all(ds, d_cc, d_inj + it_off[l] + t, WS, qd, s->class_mask, (uint32_t)t, D,
+                                                 ring_items, L.d_rad, b, sm, cs));
                      ++path_launches;
                  }
                  // carried into t + 1: the samples injected by iterations t - depth + 2 .. t
@@ -1724,7 +1792,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      }
                      HIP_OK(hipEventRecord(L.fork_ev, L0));
                      HIP_OK(hipStreamWaitEvent(S, L.fork_ev, 0));
-                     const size_t nz = timed ? 0 : n_counts;
+                     const size_t nz = counted ? 0 : n_counts;
                      HIP_OK(launch_accumulate(rk, ring_items, L.d_acc, n_pix, planes, k == 0, 1, fp, d_out, L.d_counts,
                                               (uint32_t)nz, S));
                      L.counts_clean = nz;
@@ -1826,7 +1894,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                 // the last batch's accumulate finishes the frame (into_color) and, when no statistics
                 // read the queue counters afterwards, zeroes them for the next frame (no memset launch)
                 join_to_S();
-                const size_t nz = (wavefront && !timed) ? n_counts : 0;
+                const size_t nz = (wavefront && !counted) ? n_counts : 0;
                 HIP_OK(launch_accumulate(L.d_rad, pp.n_items, L.d_acc, n_pix, nb, s0 == 0, 1, fp, d_out, L.d_counts,
                                          (uint32_t)nz, S));
                 L.counts_clean = nz;
@@ -1848,16 +1916,20 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
 // Wait for replica P's share and add its statistics into *stats (which the caller zeroed).
 void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
     if (P.empty) return;
-    if (!P.timed || !stats) { HIP_OK(hipStreamSynchronize(P.stream)); return; }
+    if (!P.counted || !stats) { HIP_OK(hipStreamSynchronize(P.stream)); return; }
     Slot& L = *P.L;
-    HIP_OK(hipMemcpyAsync(P.cnt, L.d_cnt, sizeof(P.cnt), hipMemcpyDeviceToHost, P.stream));
+    // a timed frame: the counters after everything on its stream; a counted (untimed) one, whose stream may
+    // already carry later frames in other slots (rs_render_rows' bands): the caller has waited for this
+    // frame, so its slot's counters are final and are read on the slot's own lane stream
+    const hipStream_t cs = P.timed ? P.stream : L.lane[0];
+    HIP_OK(hipMemcpyAsync(P.cnt, L.d_cnt, sizeof(P.cnt), hipMemcpyDeviceToHost, cs));
     size_t words = 0;
     if (P.N > 0 && P.kind == 2)
         for (const LaneSched& ln : P.lanes) words = std::max<size_t>(words, ln.cnt_off + (ln.T + 1) * kWfsStride);
     if (P.N > 0 && P.kind == 1) words = (size_t)P.n_chunks_total * (P.depth + 1);
     P.qc.assign(words, 0u);
-    if (words) HIP_OK(hipMemcpyAsync(P.qc.data(), L.d_counts, words * sizeof(uint32_t), hipMemcpyDeviceToHost, P.stream));
-    HIP_OK(hipStreamSynchronize(P.stream));
+    if (words) HIP_OK(hipMemcpyAsync(P.qc.data(), L.d_counts, words * sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
+    HIP_OK(hipStreamSynchronize(cs));
     double path_ms = 0.0;
     for (size_t b = 0; b + 1 < P.ev.size(); b += 2) {
         float ms = 0;
@@ -1885,9 +1957,9 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         kbytes = 80ull * seg;
     } else {
         // the streaming extend's library byte model, per iteration: ray records in (64 B)
-        // per carried path; hit (16 B) + queue slot (4 B) per shaded segment; the record out (96 B + item
-        // + level) per live camera sample (written before its traversal); radiance out (24 B) per path
-        // ending in extend, + its throughput record and item in (36 B); radiance out for masked samples
+        // per carried path; hit (16 B) + queue slot (4 B) per shaded segment (camera samples are traced
+        // from registers and write no record); radiance out (24 B) per path ending in extend, + its
+        // throughput record and item in (36 B); radiance out for masked samples
         for (size_t l = 0; l < P.lanes.size(); ++l)
             for (uint64_t t = 0; t < P.lanes[l].T; ++t) {
                 const uint32_t* q = &P.qc[P.lanes[l].cnt_off + t * kWfsStride];
@@ -1898,7 +1970,17 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
                 const uint64_t dead_new = P.inj[l][t] - live_new;
                 const uint64_t ended = live - shaded;
                 seg += live;
-                kbytes += 64ull * old + 20ull * shaded + 104ull * live_new + 60ull * ended + 24ull * dead_new;
+                kbytes += 64ull * old + 20ull * shaded + 60ull * ended + 24ull * dead_new;
+#ifdef RS_DEV_KNOBS
+                if (s->dump_iters) {
+                    const uint32_t* qn = q + kWfsStride;  // the next set's runs
+                    std::fprintf(stderr, "iter lane %zu t %3llu: carried %9llu (front %9u back %9u) camera %9llu shaded %9llu"
+                                 " [%u %u %u %u %u] ended %9llu -> next front %9u back %9u\n", l, (unsigned long long)t,
+                                 (unsigned long long)old, q[cix(kCntFront)], q[cix(kCntBack)], (unsigned long long)live_new,
+                                 (unsigned long long)shaded, q[cix(1)], q[cix(2)], q[cix(3)], q[cix(4)], q[cix(5)],
+                                 (unsigned long long)ended, qn[cix(kCntFront)], qn[cix(kCntBack)]);
+                }
+#endif
             }
         stats->kernel_id = RS_KERNEL_WFS_EXTEND;
     }
@@ -1947,7 +2029,7 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
             const RowSet rows = replica_rows(cam, st, k, n);
             DeviceGuard g(R.device);
             if (k == 0) {
-                render_enqueue(s, R, cam, st, rows, d_mask, d_out, stream, *P[k], stats != nullptr);
+                render_enqueue(s, R, cam, st, rows, d_mask, d_out, stream, *P[k], stats != nullptr, false);
                 continue;
             }
             if (rows.count() == 0) continue;
@@ -1955,7 +2037,7 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
             HIP_OK(hipStreamWaitEvent(R.stream, entry, 0));
             // this frame's copies of the mask and the frame live in R's next slot (the slot render_enqueue
             // picks): its previous frame must be done with them
-            const uint32_t n_slots = s->stack_need > stack_lds(s->scene_mode) ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            const uint32_t n_slots = frame_slots(s);
             Slot& L = R.slots[R.next_slot % n_slots];
             if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
             ensure(L, L.d_out, L.out_cap, npx * 4);
@@ -1965,7 +2047,7 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
                 HIP_OK(hipMemcpyAsync(L.d_mask, d_mask, npx, hipMemcpyDefault, R.stream));
                 m = L.d_mask;
             }
-            render_enqueue(s, R, cam, st, rows, m, L.d_out, R.stream, *P[k], stats != nullptr);
+            render_enqueue(s, R, cam, st, rows, m, L.d_out, R.stream, *P[k], stats != nullptr, false);
             HIP_OK(copy_rows(d_out, L.d_out, cam->width, rows, hipMemcpyDefault, R.stream));
             HIP_OK(hipEventRecord(L.free_ev, R.stream));  // the copy read the slot's frame
             HIP_OK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
@@ -2018,7 +2100,7 @@ void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
             rows[k] = replica_rows(cam, st, k, n);
             if (rows[k].count() == 0) continue;
             DeviceGuard g(R.device);
-            const uint32_t n_slots = s->stack_need > stack_lds(s->scene_mode) ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            const uint32_t n_slots = frame_slots(s);
             Slot& L = R.slots[R.next_slot % n_slots];
             slot[k] = &L;
             if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
@@ -2029,7 +2111,7 @@ void render_frame_host(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
                 HIP_OK(hipMemcpyAsync(L.d_mask, mask, npx, hipMemcpyHostToDevice, R.stream));
                 m = L.d_mask;
             }
-            render_enqueue(s, R, cam, st, rows[k], m, L.d_out, R.stream, *P[k], stats != nullptr);
+            render_enqueue(s, R, cam, st, rows[k], m, L.d_out, R.stream, *P[k], stats != nullptr, false);
         }
         for (uint32_t k = 0; k < n; ++k) {
             if (rows[k].count() == 0) continue;
@@ -2070,7 +2152,9 @@ void render_frame_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
     if (bands == 0) bands = 16;
     const uint32_t per = std::max<uint32_t>(1, (n_rows + bands - 1) / bands);
     const uint32_t n_bands = n_rows ? (n_rows + per - 1) / per : 0;
-    const uint32_t ahead = std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+    // bands in flight per replica: one per frame slot (a band's statistics are read from its slot's counters,
+    // so a second band in the same slot would overwrite them before render_finish reads them)
+    const uint32_t ahead = frame_slots(s);
     float* pinned = nullptr;
     std::vector<std::unique_ptr<Pending>> P(n_bands);
     std::vector<hipEvent_t> copied(n_bands, nullptr);
@@ -2102,12 +2186,12 @@ void render_frame_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
             bs.row_end = (uint32_t)std::min<uint64_t>(re, (uint64_t)bs.row_begin + (uint64_t)per * step);
             bs.row_step = step;
             rows[b] = replica_rows(cam, &bs, 0, 1);
-            const uint32_t n_slots = s->stack_need > stack_lds(s->scene_mode) ? 1u : std::max<uint32_t>(1, std::min(kMaxSlots, s->frames_in_flight));
+            const uint32_t n_slots = frame_slots(s);
             Slot& L = R.slots[R.next_slot % n_slots];
             if (L.free_rec) HIP_OK(hipStreamWaitEvent(R.stream, L.free_ev, 0));
             ensure(L, L.d_out, L.out_cap, npx * 4);
             P[b].reset(new Pending());
-            render_enqueue(s, R, cam, &bs, rows[b], d_masks[b % n], L.d_out, R.stream, *P[b], stats != nullptr);
+            render_enqueue(s, R, cam, &bs, rows[b], d_masks[b % n], L.d_out, R.stream, *P[b], false, stats != nullptr);
             HIP_OK(copy_rows(pinned, L.d_out, W, rows[b], hipMemcpyDeviceToHost, R.stream));
             HIP_OK(hipEventRecord(L.free_ev, R.stream));  // the copy read the slot's frame
             HIP_OK(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
@@ -2117,8 +2201,8 @@ void render_frame_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_s
         for (uint32_t b = 0; b < n_bands; ++b) {
             {
                 DeviceGuard g(s->reps[b % n]->device);
-                if (stats) render_finish(s, *P[b], &acc);  // (statistics: the band's share, synchronous)
                 HIP_OK(hipEventSynchronize(copied[b]));
+                if (stats) render_finish(s, *P[b], &acc);  // the band's counts (untimed: bands overlap)
             }
             if (b + ahead * n < n_bands) enqueue(b + ahead * n);
             for (uint32_t y = rows[b].begin; y < rows[b].end; y += rows[b].step) {
@@ -2195,6 +2279,8 @@ int rs_scene_create(rs_scene** out) {
         v = s->stream_lanes; knob("RS_SLANES", v); s->stream_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
         v = s->frames_in_flight; knob("RS_FRAMES", v); s->frames_in_flight = (uint32_t)std::min<unsigned long long>(v, kMaxSlots);
         v = 0; knob("RS_EXT_SPLIT", v); s->ext_split = v != 0;
+        v = 0; knob("RS_SPLIT_RUNS", v); s->split_runs = v != 0;
+        v = 0; knob("RS_DUMP_ITERS", v); s->dump_iters = v != 0;
 #endif
         *out = s;
     });

@@ -39,6 +39,10 @@ constexpr bool streaming_mode(int sm) { return sm == kSmSpheres || sm == kSmNest
 // 10 % faster although more of its deep entries spill to HBM, C4 2.5 % and example.sdl 1.6 %; the
 // rich mode (X2) lost 4 % and the spheres mode is unchanged (profiles/r4/ab/lds_stack).
 constexpr int stack_lds(int sm) { return (sm == kSmFlat || sm == kSmNest0 || sm == kSmNest2) ? kStackMin : kStackMax; }
+// the nest modes' LDS scene image (rs_layout.h kLimgMax) next to their stack: four 256-thread blocks per CU
+// must fit the CU's 160 KiB of LDS
+static_assert(4u * ((uint32_t)stack_lds(kSmNest0) * kBlock * 4u + kLimgMax) <= 160u * 1024u, "LDS image budget");
+static_assert(4u * ((uint32_t)stack_lds(kSmNest2) * kBlock * 4u + kLimgMax) <= 160u * 1024u, "LDS image budget");
 
 // A committed scene for a launch: the host copy (launch decisions) and the same struct in device
 // memory, which the kernels read through a pointer (a by-value kernel argument that device functions
@@ -98,6 +102,16 @@ struct InjParams {
     uint64_t g0, g1;      // frame items of the two batches' starts (k * batch: a lane's batches are not adjacent)
     uint32_t rad0, rad1;  // rad ring offsets of the two batches' buffers
     uint64_t ring;        // rad channel stride (ring_batches * batch items)
+    uint32_t run;         // extend: 0 every record of the launch's part; 1 the carried front run only;
+                          // 2 the rest (dev builds time the two runs in separate launches)
+};
+
+// A frame's camera and lattice in device memory (one copy per frame), next to every iteration's InjParams:
+// the shading reads them only where it regenerates a camera sample, so the kernel keeps no registers for them
+// (as kernel arguments they raised its SGPR spills 95 -> 211 and added 68 B of VGPR scratch).
+struct CamConsts {
+    DCamera C;
+    PathParams P;
 };
 
 struct FinalParams {
@@ -149,10 +163,12 @@ constexpr bool ext_split(int sm) { return sm == kSmNest2; }
 hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                              uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
                              int part, int sm, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present
-hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
-                                uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, int sm,
-                                hipStream_t st);
+// every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present; cc / inj
+// (device memory): the frame's camera and the iteration's injection (its camera samples are regenerated, not
+// read back); ring: the rad channel stride
+hipError_t launch_wfs_shade_all(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
+                                uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
+                                uint64_t ring, double* rad, uint32_t blocks, int sm, hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
 hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
 hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st);

@@ -783,35 +783,9 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
             RS_ST_NODE();
             node = bvh4_step<SM, STK, LOBJ>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
         }
-    } else if ((SM == kSmSpheres || SM == kSmFlat || SM == kSmGeneric) && !S.ref_order) {
-        // binary near-first (monotone scenes without the 4-wide tree); the nest modes use the
-        // reference order below for these too (valid for any scene, fewer inlined leaf tests)
-        while (true) {
-            const DNode N = S.nodes[node];
-            float e0, e1;
-            const int c0 = N.child[0], c1 = N.child[1];
-            bool h0 = slab32(N.lo[0], N.hi[0], rf, tmin32, best32, e0);
-            if (h0 && c0 < 0) { h0 = false; RS_LEAF(c0); }
-            bool h1 = slab32(N.lo[1], N.hi[1], rf, tmin32, best32, e1);
-            if (h1 && c1 < 0) { h1 = false; if (c1 != INT32_MIN) RS_LEAF(c1); }
-            if (h0 && h1) {
-                int nn = c0, ff = c1;
-                if (e1 < e0) { nn = c1; ff = c0; }
-                stk.put(sp, ff);
-                ++sp;
-                node = nn;
-            } else if (h0) {
-                node = c0;
-            } else if (h1) {
-                node = c1;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                node = stk.get(sp);
-            }
-        }
     } else {
-        // BVH::hit's recursion order (bvh.rs:173-192), one child per pass: k = 0 the left child,
+        // (the generic mode's reference-order scenes: boxes / quadrics / CSG in rich scenes) BVH::hit's
+        // recursion order (bvh.rs:173-192) on the binary tree, one child per pass: k = 0 the left child,
         // k = 1 the right one (its box tested with the range the left subtree left behind); an inner
         // left child is entered with the node pushed to come back for its right child. One leaf-test
         // site, so the nested-object tests are inlined once.
@@ -1209,6 +1183,14 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
     camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
     return true;
 }
+// camera_sample of an item known to be live (the shading's regeneration of a traced camera sample)
+__device__ __forceinline__ void camera_sample_xy_item(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
+    const uint32_t pl = (uint32_t)(item % P.n_pix_local);
+    const uint32_t sl = (uint32_t)(item / P.n_pix_local);
+    const uint32_t x = pl % P.width;
+    const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
+    camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
+}
 
 // Camera-ray order: the i-th camera sample a launch traces is item gen_perm(i) of its batch (whole
 // sample planes). Within each plane the lattice pixels are visited in TW x TH tiles (TW * TH = 64:
@@ -1244,6 +1226,20 @@ __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_
         }
     }
     return s * npl + pl;
+}
+
+// The camera sample behind the streaming iteration's injected record jg (0-based among its injections):
+// its frame item g (camera_sample) and its radiance slot in the rad ring. The extend generates the sample
+// from it and the shading regenerates it the same way (no path record is written for a camera sample).
+__device__ __forceinline__ void inj_sample(const InjParams& I, const PathParams& P, uint32_t jg, uint64_t& g,
+                                           uint32_t& item) {
+    uint32_t jb = I.jb0 + jg, nb = I.nb0;
+    uint64_t g0 = I.g0;
+    item = I.rad0;
+    if (jb >= I.nb0) { jb -= I.nb0; nb = I.nb1; g0 = I.g1; item = I.rad1; }
+    const uint32_t perm = gen_perm(jb, 0, nb, P);
+    item += perm;
+    g = g0 + perm;
 }
 
 #if RS_TU_COMMON
@@ -1414,7 +1410,11 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
     const uint32_t n = n_old + (PART == kExtCarried ? 0u : I.n_new);
     if (PART != kExtCamera && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n_old;  // paths carried in (stats)
     const WfSet& cur = W.set[it & 1];
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    // the records of this launch: all, or (I.run, dev timing) the carried front run / the rest
+    const uint32_t j_lo = (PART != kExtCamera && I.run == 2) ? min(nf, n) : 0u;
+    const uint32_t j_hi = (PART != kExtCamera && I.run == 1) ? min(nf, n) : n;
+    const uint32_t base0 = j_lo + blockIdx.x * kBlock;
+    for (uint32_t base = base0; base < j_hi; base += gridDim.x * kBlock) {
         // thread -> record: the front run [0, nf), the back run from the set's end down, then the
         // injected camera samples, whose records follow the front run
         const uint32_t j = base + threadIdx.x;
@@ -1425,15 +1425,11 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
         Ray r;
         Rng rng;
         uint32_t item = 0;
-        if (j < n) {
+        if (j < j_hi) {
             if (gen) {
-                uint32_t jb = I.jb0 + (j - n_old), nb = I.nb0;
-                uint64_t g0 = I.g0;
-                item = I.rad0;
-                if (jb >= I.nb0) { jb -= I.nb0; nb = I.nb1; g0 = I.g1; item = I.rad1; }
-                const uint32_t perm = gen_perm(jb, 0, nb, P);
-                item += perm;
-                live = camera_sample(C, P, g0 + perm, r, rng);
+                uint64_t g;
+                inj_sample(I, P, j - n_old, g, item);
+                live = camera_sample(C, P, g, r, rng);
                 if (!live) { rad[item] = 0.0; rad[I.ring + item] = 0.0; rad[2 * I.ring + item] = 0.0; }
             } else {
                 r = load_ray(cur, i);
@@ -1443,7 +1439,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
         // the LDS image is filled once the block's first records are requested: their latency and the
         // image's overlap at the barrier
         if constexpr (LOBJ)
-            if (base == blockIdx.x * kBlock) lds_fill(S);
+            if (base == base0) lds_fill(S);
         if (live) {
             double bend = RS_INF;
             const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ>(S, r, 0.0001, bend, stk);
@@ -1477,10 +1473,12 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
                     add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
                     cls = -1;
                 } else {
+                    // a carried path's record is in place; a camera sample that goes on to shading has
+                    // none (T = 1, level 0): the shading regenerates it from its slot (inj_sample)
                     W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-                    // a camera sample that goes on to shading: its record (T = 1, level 0); a carried
-                    // path's is in place
+#ifdef RS_CAM_RECORDS  // dev A/B: the camera sample's record written here and read back by the shading
                     if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
+#endif
                     done = false;
                 }
             }
@@ -1513,10 +1511,16 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
 // One batch of 256 queued paths of material class KIND (-1: the generic material switch; entries
 // base .. base + 255 of a queue of n): finish the hit record, scatter, write the radiance of paths that
 // end and append the survivors to the next set. Must be called by every thread of the block (block_slot).
+// Camera samples injected by the iteration (records nf .. nf + I.n_new - 1 of the set, nf = its front run)
+// have no record: the extend traced them from registers, and here they are regenerated from their slot
+// (inj_sample + camera_sample: the same ray and RNG state, T = 1, level 0) instead of being written and
+// read back (104 B each way per camera sample that reaches a surface).
 template <int KIND, int SM>
 __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const uint32_t* __restrict__ queue,
-                                                uint32_t n, uint32_t base, uint32_t it, uint32_t* cnt_next, uint32_t depth,
-                                                uint64_t ring, double* __restrict__ rad) {
+                                                uint32_t n, uint32_t base, uint32_t it, uint32_t nf, uint32_t* cnt_next,
+                                                uint32_t depth, uint64_t ring, double* __restrict__ rad,
+                                                const CamConsts* __restrict__ cc, const InjParams* __restrict__ inj,
+                                                uint32_t n_new) {
     const WfSet& cur = W.set[it & 1];
     const WfSet& nxt = W.set[(it + 1) & 1];
     const uint32_t j = base + threadIdx.x;
@@ -1528,14 +1532,30 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     uint32_t item = 0, lvl = 0;
     if (j < n) {
         const uint32_t i = queue[j];
-        load_path(cur, i, r, T, rng);
+        const uint32_t jg = i - nf;
+#if defined(RS_CAM_RECORDS)
+        if (false) {
+#elif defined(RS_CAM_FAKE)  // dev bound: no record read and no regeneration (wrong frames)
+        if (jg < n_new) {
+            item = jg; r.o = v3((double)i, 1.0, 2.0); r.d = v3(0.0, 1.0, 0.0); r.time = 0.0; rng.x = rng.y = rng.z = rng.w = jg | 1u;
+            T = v3(1.0, 1.0, 1.0);
+#else
+        if (jg < n_new) {
+            uint64_t g;
+            inj_sample(*inj, cc->P, jg, g, item);
+            camera_sample_xy_item(cc->C, cc->P, g, r, rng);
+            T = v3(1.0, 1.0, 1.0);
+#endif
+        } else {
+            load_path(cur, i, r, T, rng);
+            const uint2 tg = cur.tag[i];
+            item = tg.x;
+            lvl = tg.y;
+        }
         const double2 hb = W.hit[i];
         const int bp = (int)__double_as_longlong(hb.x);
         Hit h;
         finish_hit<SM, (KIND >= 0)>(S, bp, r, 0.0001, hb.y, h);
-        const uint2 tg = cur.tag[i];
-        item = tg.x;
-        lvl = tg.y;
         const int mi = h.mat >= 0 ? h.mat : S.default_mat;
         const DMaterial& M0 = S.mats[mi];
         bool cont;
@@ -1586,13 +1606,17 @@ __global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) vo
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
-                                                                                   double* __restrict__ rad) {
+                                                                                   double* __restrict__ rad,
+                                                                                   const CamConsts* __restrict__ cc,
+                                                                                   const InjParams* __restrict__ inj) {
     // (3 waves: 171 -> 168 VGPRs; at 4 waves it spilled 156 B, +6 %; nest-2 bounded at 3 spilled: C4 -21 %)
     DScene Sv;
     if constexpr (LOBJ) lds_scene(Sp, Sv);
     const DScene& S = LOBJ ? Sv : *Sp;
     const uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
     uint32_t* cnt_next = W.counts + (size_t)(it + 1) * kWfsStride;
+    const uint32_t nf = cnt[cix(kCntFront)];  // the front run: the injected camera samples' slots follow it
+    const uint32_t n_new = inj->n_new;
     constexpr int NC = G4 ? 5 : 4;
     uint32_t n[NC], first[NC + 1];
     first[0] = 0;
@@ -1607,15 +1631,15 @@ __global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) vo
         for (int c = 1; c < NC; ++c) k += v >= first[c] ? 1 : 0;
         const uint32_t base = (v - first[k]) * kBlock;
         if (k == 0)
-            wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], n[0], base, it, cnt_next, depth, ring, rad);
+            wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], n[0], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
         else if (k == 1)
-            wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], n[1], base, it, cnt_next, depth, ring, rad);
+            wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], n[1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
         else if (k == 2)
-            wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], n[2], base, it, cnt_next, depth, ring, rad);
+            wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], n[2], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
         else if (k == 3 || !G4)
-            wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], n[3], base, it, cnt_next, depth, ring, rad);
+            wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], n[3], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
         else
-            wfs_shade_batch<-1, SM>(S, W, queues[NC - 1], n[NC - 1], base, it, cnt_next, depth, ring, rad);
+            wfs_shade_batch<-1, SM>(S, W, queues[NC - 1], n[NC - 1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
     }
 }
 
@@ -1799,10 +1823,10 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
                                uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, \
                                int part, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1),                        \
       (s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1))                                                  \
-    X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, \
-                                  uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks,       \
-                                  hipStream_t st),                                                              \
-      (s, w, queues, class_mask, it, depth, ring, rad, blocks, st))
+    X(hipError_t, wfs_shade_all, (const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w, \
+                                  uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,      \
+                                  uint64_t ring, double* rad, uint32_t blocks, hipStream_t st),                   \
+      (s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks, st))
 #define RS_DECLARE_SM(R, NAME, PARAMS, ARGS) template <int SMC> R NAME##_sm PARAMS;
 RS_SM_LAUNCHERS(RS_DECLARE_SM)
 RS_SORTED_LAUNCHERS(RS_DECLARE_SM)
@@ -1886,12 +1910,13 @@ hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& 
 }
 
 template <int SMC>
-hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, uint32_t it,
-                            uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, hipStream_t st) {
+hipError_t wfs_shade_all_sm(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
+                            uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
+                            uint64_t ring, double* rad, uint32_t blocks, hipStream_t st) {
     if (!blocks) return hipSuccess;
 #define RS_SHADE_LAUNCH(G4, LOBJ, SHM)                                                                              \
     hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, queues, class_mask, \
-                       it, depth, ring, rad)
+                       it, depth, ring, rad, cc, inj)
     const uint32_t shm = s.host->limg_bytes;  // nest modes' LDS image (none in the spheres mode)
     if constexpr (SMC == kSmNest0 || SMC == kSmNest2) {
         if (class_mask & (1u << 4)) { if (shm) RS_SHADE_LAUNCH(true, true, shm); else RS_SHADE_LAUNCH(true, false, 0); }
@@ -1959,10 +1984,10 @@ hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathPara
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
-                                uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, int sm,
-                                hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, it, depth, ring, rad, blocks, st));
+hipError_t launch_wfs_shade_all(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
+                                uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
+                                uint64_t ring, double* rad, uint32_t blocks, int sm, hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks, st));
     return hipErrorInvalidValue;
 }
 

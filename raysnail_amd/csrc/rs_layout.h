@@ -158,8 +158,9 @@ struct DBox64 {    // an object's reference bbox (exact f64), tested before its 
 // tables of the LDS image (DScene::limg_off), in image order
 enum LimgTable { LT_NODES4 = 0, LT_PBOX, LT_PCLASS, LT_PRIMS, LT_SPHERES, LT_RECTS, LT_BOXES, LT_QUADRICS, LT_CSGS,
                  LT_XFORMS, LT_TF_FWD, LT_TF_INV, LT_COUNT };
-// LDS bytes the image may take: the nest-0 extend keeps 4 blocks of 256 per CU, each with its
-// 24 KiB traversal stack (4 x (24 + 15) KiB <= 160 KiB)
+// LDS bytes the image may take: the nest-mode extend keeps 4 blocks of 256 per CU, each with its
+// 16-entry traversal stack (stack_lds: 16 KiB) and the image, 4 x (16 + 15) KiB = 124 KiB <= 160 KiB
+// (rs_internal.h checks it against the CU's LDS)
 constexpr uint32_t kLimgMax = 15u * 1024u;
 
 struct DScene {

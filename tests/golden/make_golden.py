@@ -27,6 +27,8 @@ FRAMES = {
     "quadric_sdl": (lambda: scenes.quadric_sdl(48, 48), 16, 8, 1),
     "cornell": (lambda: scenes.cornell_box(40, 40), 16, 8, 1),
     "rtow_depth50": (lambda: scenes.rtow_13_1(32, 20)[:2], 9, 50, 3),
+    # BASELINE config C1 exactly: examples/rtow_13_1.rs's scene at 400x225, 16 spp, depth 8
+    "rtow_c1": (lambda: scenes.rtow_13_1(400, 225)[:2], 16, 8, 1),
 }
 
 

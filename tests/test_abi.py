@@ -208,3 +208,69 @@ def test_integration_declares_every_export():
         n_c = 0 if args.strip() in ("", "void") else args.count(",") + 1
         n_r = 0 if not rust[name].strip() else rust[name].count(",") + 1
         assert n_c == n_r, name
+
+
+def _rust_ffi_block():
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = text[text.index("```rust"):]
+    return block[:block.index("```", 7)]
+
+
+def _c_param_type(decl):
+    """a C parameter declaration -> the Rust type a #[repr(C)] binding must give it"""
+    base = {"uint32_t": "u32", "int32_t": "i32", "uint64_t": "u64", "int64_t": "i64", "double": "f64", "float": "f32",
+            "uint8_t": "u8", "int": "i32", "void": "c_void", "char": "c_char", "rs_scene": "RsScene",
+            "rs_row_callback": "RsRowCallback"}
+    base.update({c: r for r, c in C_OF_RUST.items()})
+    decl = decl.strip()
+    arr = re.search(r"\[\d+\]\s*$", decl)
+    decl = re.sub(r"\[\d+\]\s*$", "", decl)
+    toks = decl.replace("*", " * ").split()
+    const = toks[0] == "const"
+    if const:
+        toks = toks[1:]
+    stars = toks.count("*") + (1 if arr else 0)
+    t = base[toks[0]]
+    for k in range(stars):
+        t = ("*const " if (const and k == 0) else "*mut ") + t
+    return t
+
+
+def _rust_type(t):
+    t = t.strip().replace("std::ffi::c_void", "c_void").replace("std::os::raw::c_char", "c_char")
+    return "*mut c_void" if t == "HipStream" else t
+
+
+def test_integration_ffi_types_match_c():
+    """Every function of INTEGRATION.md's FFI block has the header's parameter types in order (and its return
+    type): const T* <-> *const T, T* <-> *mut T, fixed arrays as pointers, hipStream_t (void*) as HipStream."""
+    block = _rust_ffi_block()
+    rust = {m.group(1): (m.group(2), m.group(3)) for m in
+            re.finditer(r"pub fn (rs_\w+)\((.*?)\)\s*(?:->\s*([^;]*))?;", block, flags=re.S)}
+    hdr = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "raysnail_hip.h")).read(), flags=re.S)
+    hdr = re.sub(r"typedef void \(\*rs_row_callback\)\([^)]*\);", "", hdr)
+    for m in re.finditer(r"([\w\s\*]+?)\b(rs_[a-z_0-9]+)\s*\(([^)]*)\)\s*;", hdr):
+        ret, name, args = m.group(1).strip(), m.group(2), m.group(3)
+        c_params = [] if args.strip() in ("", "void") else [_c_param_type(a.rsplit(None, 1)[0] if not re.search(r"\[\d+\]$", a.strip()) else re.sub(r"\w+\s*(\[\d+\])$", r"\1", a.strip())) for a in args.split(",")]
+        r_args, r_ret = rust[name]
+        r_params = [_rust_type(a.split(":", 1)[1]) for a in r_args.split(",") if a.strip()]
+        assert c_params == r_params, (name, c_params, r_params)
+        c_ret = _c_param_type(ret) if ret not in ("int",) else "i32"
+        assert c_ret == _rust_type(r_ret or ""), (name, c_ret, r_ret)
+
+
+def test_integration_row_callback_matches_c():
+    """RsRowCallback (the Rust side of rs_row_callback) and the drop-in's forward_row trampoline (INTEGRATION.md
+    §3) have the header typedef's parameter types, and the drop-in renders through rs_render_rows (rows delivered
+    as their bands finish, painter.rs:214, then the sentinel, painter.rs:332), not rs_render."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    hdr = open(os.path.join(ROOT, "include", "raysnail_hip.h")).read()
+    c_args = re.search(r"typedef void \(\*rs_row_callback\)\(([^)]*)\);", hdr).group(1)
+    c_params = [_c_param_type(a.rsplit(None, 1)[0]) for a in c_args.split(",")]
+    alias = re.search(r"pub type RsRowCallback = extern \"C\" fn\(([^)]*)\);", _rust_ffi_block()).group(1)
+    assert [_rust_type(a.split(":", 1)[1]) for a in alias.split(",")] == c_params
+    sec3 = text[text.index("## 3. The drop-in call"):text.index("## 4. Multi-GPU")]
+    tramp = re.search(r"extern \"C\" fn forward_row\(([^)]*)\)", sec3).group(1)
+    assert [_rust_type(a.split(":", 1)[1]) for a in tramp.split(",")] == c_params
+    assert "rs_render_rows(" in sec3 and "forward_row" in sec3.split("rs_render_rows(", 1)[1]
+    assert "rs_render(" not in sec3.replace("rs_render_rows(", "")

@@ -41,7 +41,7 @@ def _load_make_golden():
     return mg
 
 
-@pytest.mark.parametrize("name", ["rtow", "example_sdl", "quadric_sdl", "cornell", "rtow_depth50"])
+@pytest.mark.parametrize("name", ["rtow", "example_sdl", "quadric_sdl", "cornell", "rtow_depth50", "rtow_c1"])
 def test_golden_frames(gpu, name):
     mg = _load_make_golden()
     build, spp, depth, seed = mg.FRAMES[name]

@@ -13,6 +13,10 @@
 #            on the bench frame, C4's and C5's scenes
 #   scenes   kernel traces of the C4 / C5 scenes (tools/time_scene.py)
 #   configs  tools/bench_configs.py (C2-C5, X1, X2 vs the CPU oracle on row subsets)
+#   ab       bench.py of this tree against the baseline worktree base/, 3 rounds interleaved (tools/ab_report.py)
+#   variants bench.py of base/, the product and every raysnail_amd/lib/var_*.so (tools/build_variant.sh), 2 rounds
+#   abtrace  kernel traces of the bench frames, base/ then this tree (tools/trace_cmp.py)
+#   iters    per-iteration queue counts + per-run extend launches of the bench frame (dev library; tools/iter_table.py)
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=$1; shift
@@ -55,6 +59,36 @@ for s in "$@"; do
   scenes)
     (cd /tmp && step 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tr_c4 -o tr -- python3 $R/tools/time_scene.py default quadric 16 50 1024x1024 > $OUT/tr_c4.log 2>&1) || { echo "c4 trace failed"; tail -5 $OUT/tr_c4.log; exit 1; }
     (cd /tmp && step 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tr_c5 -o tr -- python3 $R/tools/time_scene.py default mesh 16 50 1920x1080 > $OUT/tr_c5.log 2>&1) || { echo "c5 trace failed"; tail -5 $OUT/tr_c5.log; exit 1; } ;;
+  ab)
+    # this tree's bench line against the baseline worktree base/ (tools/ab_base.sh), 3 rounds interleaved
+    for rep in 1 2 3; do
+      (cd $R/base && step 240 python3 bench.py --cpu-baseline 0 --steps 20 --warmup 5 > $OUT/ab_base_$rep.json 2> $OUT/ab_base.err) || { echo "base bench failed"; tail -5 $OUT/ab_base.err; exit 1; }
+      (cd $R && step 240 python3 bench.py --cpu-baseline 0 --steps 20 --warmup 5 > $OUT/ab_new_$rep.json 2> $OUT/ab_new.err) || { echo "bench failed"; tail -5 $OUT/ab_new.err; exit 1; }
+    done
+    (cd $R && python3 tools/ab_report.py $OUT/ab_base_*.json -- $OUT/ab_new_*.json | tee $OUT/ab.txt) ;;
+  variants)
+    # bench.py of base/, this tree's product and every dev variant (raysnail_amd/lib/var_*.so, tools/build_variant.sh),
+    # 2 rounds interleaved; frames of the variants are not checked here (dev bounds may be wrong on purpose)
+    B="--cpu-baseline 0 --steps 20 --warmup 5"
+    for rep in 1 2; do
+      (cd $R/base && step 240 python3 bench.py $B > $OUT/v_base_$rep.json 2> $OUT/v.err) || { echo "base bench failed"; tail -5 $OUT/v.err; exit 1; }
+      (cd $R && step 240 python3 bench.py $B > $OUT/v_prod_$rep.json 2> $OUT/v.err) || { echo "bench failed"; tail -5 $OUT/v.err; exit 1; }
+      for v in $R/raysnail_amd/lib/var_*.so; do
+        n=$(basename $v .so)
+        (cd $R && RS_HIP_LIB=$v step 240 python3 bench.py $B > $OUT/v_${n}_$rep.json 2> $OUT/v.err) || { echo "$n bench failed"; tail -5 $OUT/v.err; exit 1; }
+      done
+    done
+    (cd $R && python3 tools/ab_report.py $OUT/v_*.json | tee $OUT/variants.txt) ;;
+  abtrace)
+    # kernel traces of the bench frames (tools/render_once.py, 5 frames): the baseline worktree base/, then this tree
+    (cd /tmp && step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/abt_base -o t -- python3 $R/base/tools/render_once.py 0 5 > $OUT/abt_base.log 2>&1) || { echo "base trace failed"; exit 1; }
+    (cd /tmp && step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/abt_new -o t -- python3 $R/tools/render_once.py 0 5 > $OUT/abt_new.log 2>&1) || { echo "trace failed"; exit 1; }
+    (cd $R && python3 tools/trace_cmp.py $OUT/abt_base/t_kernel_trace.csv $OUT/abt_new/t_kernel_trace.csv | tee $OUT/abtrace.txt) ;;
+  iters)
+    # one lane, the dev library: per-iteration queue counts (RS_DUMP_ITERS) and the carried front run / the
+    # rest in separate extend launches (RS_SPLIT_RUNS) under a kernel trace; then the per-launch table
+    (cd /tmp && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_DUMP_ITERS=1 RS_SPLIT_RUNS=1 step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/iters -o it -- python3 $R/tools/render_once.py 0 4 > $OUT/iters.log 2>&1) || { echo "iters trace failed"; tail -5 $OUT/iters.log; exit 1; }
+    (cd $R && python3 tools/iter_table.py $OUT/iters.log $(ls $OUT/iters/*kernel_trace.csv) | tee $OUT/iters.txt) ;;
   configs)
     (cd $R && step 900 python3 tools/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err) || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
     cat $OUT/configs.jsonl ;;
