@@ -481,3 +481,22 @@ def test_render_rows_progressive(gpu, frames):
             assert seen == list(range(lattice[0], 100, lattice[2])) + [100]
             assert np.array_equal(img[lattice[0]::lattice[2]], one[lattice[0]::lattice[2]])
     ds.set_frames_in_flight(2)
+
+
+def test_render_rows_stats_on_spilling_mesh(gpu):
+    """rs_render_rows with statistics on a tree whose traversal stack spills to HBM (one frame slot per replica):
+    every band's counters are its own (a band is not enqueued into a slot whose previous band's counters are still
+    to be read), so the summed segments and samples equal rs_render's for the same frame, and the frame is the same."""
+    cam, world = scenes.mesh_scene(96, 54)
+    ds = world.device_scene()
+    inf = ds.info()
+    assert inf.stack_need > inf.stack_lds, (inf.stack_need, inf.stack_lds)  # the spilling case
+    ds.set_frames_in_flight(2)
+    st = cam.take_photo().samples(4).depth(8).seed(3).settings()
+    ref, rst = ds.render(cam.desc, st)
+    rows = []
+    img, bst = ds.render_rows(cam.desc, st, lambda y, out: rows.append(y), None, bands=5, stats=True)
+    assert rows == list(range(54)) + [54]
+    assert np.array_equal(img, ref)
+    assert (bst.samples, bst.segments) == (rst.samples, rst.segments)
+    assert bst.kernel_bytes == rst.kernel_bytes

@@ -15,6 +15,7 @@
 #   configs  tools/bench_configs.py (C2-C5, X1, X2 vs the CPU oracle on row subsets)
 #   ab       bench.py of this tree against the baseline worktree base/, 3 rounds interleaved (tools/ab_report.py)
 #   variants bench.py of base/, the product and every raysnail_amd/lib/var_*.so (tools/build_variant.sh), 2 rounds
+#   travstats per-category traversal counters (raysnail_amd/lib/trav_stats.so, a -DRS_TRAV_STATS build)
 #   abtrace  kernel traces of the bench frames, base/ then this tree (tools/trace_cmp.py)
 #   iters    per-iteration queue counts + per-run extend launches of the bench frame (dev library; tools/iter_table.py)
 set -u
@@ -77,8 +78,33 @@ for s in "$@"; do
         n=$(basename $v .so)
         (cd $R && RS_HIP_LIB=$v step 240 python3 bench.py $B > $OUT/v_${n}_$rep.json 2> $OUT/v.err) || { echo "$n bench failed"; tail -5 $OUT/v.err; exit 1; }
       done
+      # DEVCFGS="KNOB=v,KNOB=v;KNOB=v": dev-library configurations (rs_host.cpp RS_DEV_KNOBS), one per ';'
+      IFS=';' read -ra CFGS <<< "${DEVCFGS:-}"
+      for cfg in "${CFGS[@]}"; do
+        n=dev_$(echo $cfg | tr ',=' '__')
+        (cd $R && env RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so $(echo $cfg | tr ',' ' ') timeout -k 10 240 python3 bench.py $B > $OUT/v_${n}_$rep.json 2> $OUT/v.err) || { echo "$n bench failed"; tail -5 $OUT/v.err; exit 1; }
+      done
     done
     (cd $R && python3 tools/ab_report.py $OUT/v_*.json | tee $OUT/variants.txt) ;;
+  travstats)
+    # node steps / leaf tests per ray and per wave by ray category (a -DRS_TRAV_STATS build renamed to
+    # raysnail_amd/lib/trav_stats.so: tools/build_variant.sh stats -DRS_TRAV_STATS)
+    (cd $R && step 300 python3 tools/trav_stats.py $R/raysnail_amd/lib/trav_stats.so rtow,example,quadric,mesh > $OUT/trav_stats.txt 2>&1) || { echo "trav stats failed"; tail -5 $OUT/trav_stats.txt; exit 1; }
+    cat $OUT/trav_stats.txt ;;
+  pool)
+    # C3 / C4-shaped frames with the dev library at several streaming pool sizes (RS_POOL_PATHS): iterations vs launch size
+    for pp in 67108864 134217728 268435456; do
+      for sc in "rtow 256 50 1920x1080" "quadric 64 50 1024x1024"; do
+        (cd $R && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_POOL_PATHS=$pp step 300 python3 tools/time_scene.py $R/raysnail_amd/lib/libraysnail_hip_dev.so $sc >> $OUT/pool.jsonl 2>> $OUT/pool.err) || { echo "pool $pp $sc failed"; tail -5 $OUT/pool.err; exit 1; }
+        echo "pool $pp: $(tail -1 $OUT/pool.jsonl)"
+      done
+    done ;;
+  c4)
+    # C4-shaped frames (quadric.sdl + Cornell emitter 1024x1024, 64 spp, depth 50) with the product and every variant
+    for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      (cd $R && step 300 python3 tools/time_scene.py $v quadric 64 50 1024x1024 >> $OUT/c4.jsonl 2>> $OUT/c4.err) || { echo "c4 $v failed"; tail -5 $OUT/c4.err; exit 1; }
+      echo "c4: $(tail -1 $OUT/c4.jsonl)"
+    done ;;
   abtrace)
     # kernel traces of the bench frames (tools/render_once.py, 5 frames): the baseline worktree base/, then this tree
     (cd /tmp && step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/abt_base -o t -- python3 $R/base/tools/render_once.py 0 5 > $OUT/abt_base.log 2>&1) || { echo "base trace failed"; exit 1; }

@@ -47,8 +47,8 @@ def main():
                 t += 1
                 es = []
     counts = frames[-1] if frames else []
-    print(f"{'t':>2} {'front':>9} {'back':>9} {'camera':>9} {'shaded':>9} {'ended':>9} | {'ext front us':>12} {'ns/ray':>7} "
-          f"{'ext rest us':>12} {'ns/ray':>7} {'shade us':>9} {'ns/path':>7}")
+    print(f"{'t':>2} {'front':>9} {'back':>9} {'camera':>9} {'shaded':>9} {'ended':>9} | {'ext front us':>12} {'ps/ray':>7} "
+          f"{'ext rest us':>12} {'ps/ray':>7} {'shade us':>9} {'ps/path':>7}")
     tot = defaultdict(float)
     for t in sorted(per_it):
         es = per_it[t]["E"]
@@ -64,8 +64,8 @@ def main():
             ef, er = 0.0, ext[0]
             rest = front + back + cam
         tot["ef"] += ef; tot["er"] += er; tot["sh"] += sh
-        print(f"{t:>2} {front:>9} {back:>9} {cam:>9} {shaded:>9} {ended:>9} | {ef:>12.1f} {1e3 * ef / max(front, 1):>7.1f} "
-              f"{er:>12.1f} {1e3 * er / max(rest, 1):>7.1f} {sh:>9.1f} {1e3 * sh / max(shaded, 1):>7.1f}")
+        print(f"{t:>2} {front:>9} {back:>9} {cam:>9} {shaded:>9} {ended:>9} | {ef:>12.1f} {1e6 * ef / max(front, 1):>7.1f} "
+              f"{er:>12.1f} {1e6 * er / max(rest, 1):>7.1f} {sh:>9.1f} {1e6 * sh / max(shaded, 1):>7.1f}")
     print(f"frame: extend front {tot['ef']:.1f} us, extend rest {tot['er']:.1f} us, shading {tot['sh']:.1f} us "
           f"({len(fl) - 1} frames averaged)")
 

@@ -1,4 +1,7 @@
-# dev: traversal counters of the bench frame from a -DRS_TRAV_STATS build (tools/build_variant.sh stats -DRS_TRAV_STATS)
+# dev: traversal counters of the bench frame (and other scenes) from a -DRS_TRAV_STATS build
+# (tools/build_variant.sh stats -DRS_TRAV_STATS), per ray category: camera rays (and the bounce-synchronous
+# wavefront's rays), the carried front run (light-sample rays), the rest (BSDF / other rays).
+# usage: python tools/trav_stats.py [lib.so] [scene,scene,...]
 import ctypes as C, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -8,25 +11,33 @@ _abi.lib_path = lambda: lib_file
 import torch; torch.cuda.set_device(0)
 from raysnail_amd import scenes
 lib = _abi.load()
-out = (C.c_ulonglong * 32)()
-CASES = {"rtow": (lambda: scenes.rtow_13_1(800, 500)[:2], 64, 8),
-         "mesh": (lambda: scenes.mesh_scene(960, 540), 16, 50),
-         "example": (lambda: scenes.example_sdl(800, 500), 16, 50),
-         "quadric": (lambda: scenes.quadric_sdl(512, 512), 16, 50)}
+out = (C.c_ulonglong * 128)()
+# scene -> (builder, spp, depth, translation unit of its scene mode: rs_kernels.hip RS_TU)
+CASES = {"rtow": (lambda: scenes.rtow_13_1(800, 500)[:2], 64, 8, 1),
+         "mesh": (lambda: scenes.mesh_scene(960, 540), 16, 50, 2),
+         "example": (lambda: scenes.example_sdl(800, 500), 16, 50, 3),
+         "quadric": (lambda: scenes.quadric_sdl(512, 512), 16, 50, 4)}
+CATS = ["camera/bsync", "front(light)", "rest(bsdf)"]
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["rtow"]
 for name in names:
-    build, spp, depth = CASES[name]
+    build, spp, depth, tu = CASES[name]
+    fn = getattr(lib, f"rs_debug_trav_stats_{tu}")
     cam, world = build()
     photo = cam.take_photo().samples(spp).depth(depth).seed(1)
     photo.shot(None, world)
-    lib.rs_debug_trav_stats(out, 1)
+    fn(out, 1)
     photo.shot(None, world)
-    lib.rs_debug_trav_stats(out, 1)
-    nodes, leaves, rays, wmax, lanes, waves, witer = out[:7]
-    print(f"{name}: rays {rays} nodes/ray {nodes/max(rays,1):.2f} leaves/ray {leaves/max(rays,1):.2f} "
-          f"wave-max nodes {wmax/max(waves,1):.2f} live lanes/wave {lanes/max(waves,1):.1f} "
-          f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f} "
-          f"leaf passes/wave {witer/max(waves,1):.2f} leaf-pass lane use {leaves/max(64*witer,1):.3f}", flush=True)
-    hist = list(out[8:24])
-    tot = max(1, sum(hist))
-    print("  node steps per ray, 8-wide buckets (%):", " ".join(f"{8*b}:{100*h/tot:.1f}" for b, h in enumerate(hist)), flush=True)
+    fn(out, 1)
+    for c, cname in enumerate(CATS):
+        v = out[32 * c:32 * c + 32]
+        nodes, leaves, rays, wmax, lanes, waves, witer = v[:7]
+        if not rays:
+            continue
+        print(f"{name} {cname:13s}: rays {rays} nodes/ray {nodes/max(rays,1):.2f} leaves/ray {leaves/max(rays,1):.2f} "
+              f"wave-max nodes {wmax/max(waves,1):.2f} live lanes/wave {lanes/max(waves,1):.1f} "
+              f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f} "
+              f"leaf passes/wave {witer/max(waves,1):.2f} leaf-pass lane use {leaves/max(64*witer,1):.3f}", flush=True)
+        hist = list(v[8:24])
+        tot = max(1, sum(hist))
+        print("   node steps per ray, 8-wide buckets (%):", " ".join(f"{8*b}:{100*h/tot:.1f}" for b, h in enumerate(hist)),
+              flush=True)
