@@ -154,6 +154,14 @@ __device__ __forceinline__ bool sphere_hit(const DSphere& s, int32_t mat, const 
     return true;
 }
 
+// Sphere::hit's record (sphere_hit) for the root t the traversal already chose (sphere_t's arithmetic: the
+// same t bit for bit): the point, the normal from the static center, the front-face flip. t2 is left at
+// RS_FMAX: only CSG decisions read it, and the spheres scene mode that uses this has none.
+__device__ __forceinline__ void sphere_rec_at(const DSphere& s, int32_t mat, const Ray& r, double t, Hit& h) {
+    const V3 p = ray_at(r, t);
+    finish_rec(h, r, t, RS_FMAX, sphere_normal(s, p), mat);
+}
+
 // rect.rs:101-120
 __device__ __forceinline__ bool rect_hit_raw(int ax0, int ax1, int ax2, double k, double a0, double a1, double b0, double b1,
                                              int32_t mat, const Ray& r, double tmin, double tmax, Hit& h, int uv = 0) {

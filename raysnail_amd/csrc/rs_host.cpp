@@ -282,6 +282,7 @@ struct rs_scene {
     uint32_t stream_lanes = 1;                    // lanes of the streaming wavefront (rs_scene_set_lanes)
     uint32_t frames_in_flight = 2;                // frame slots per replica (rs_scene_set_frames_in_flight)
     bool ext_split = false;                       // streaming extend in two launches per iteration in every mode (dev A/B)
+    bool shade_split = true;                      // spheres mode: lean / heavy material classes in two shading launches
     bool split_runs = false;                      // dev: carried front run / the rest in separate extend launches
     bool dump_iters = false;                      // dev: per-iteration queue counts to stderr (timed frames)
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
@@ -1739,7 +1740,11 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  // kernel compiled for that part alone (example.sdl 8.95 -> 8.41 ms); the spheres mode
                  // keeps the merged kernel (its parts measured 2.8 % slower on the bench frame:
                  // profiles/r4/ab/part_pick)
+#ifdef RS_EXT_W5  // dev A/B: the spheres mode picks the part kernels too (its carried part runs at 5 waves)
+                 const bool pick = true;
+#else
                  const bool pick = sm != kSmSpheres;
+#endif
 #ifdef RS_DEV_KNOBS
                  if (s->split_runs && n_new == 0 && !split && window[l]) {  // dev: the front run and the rest timed apart
                      I.run = 1;
@@ -1761,8 +1766,13 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  }
                  if (D > 0) {
                      const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + n_new + kBlock - 1) / kBlock);
+#ifdef RS_CAM_RECORDS  // dev A/B: the extend wrote the camera samples' records
+                     const bool cam = false;
+#else
+                     const bool cam = n_new > 0;
+#endif
                      HIP_OK(launch_wfs_shade_all(ds, d_cc, d_inj + it_off[l] + t, WS, qd, s->class_mask, (uint32_t)t, D,
-                                                 ring_items, L.d_rad, b, sm, cs));
+                                                 ring_items, L.d_rad, b, cam, s->shade_split, sm, cs));
                      ++path_launches;
                  }
                  // carried into t + 1: the samples injected by iterations t - depth + 2 .. t
@@ -1776,7 +1786,11 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  // batch k's samples have all finished: accumulate in sample order (the last batch on S,
                  // writing the frame and zeroing the counters for the next frame unless statistics read them)
                  const uint32_t planes = (uint32_t)(std::min<uint64_t>(f.B, (uint64_t)n_pix * N - (uint64_t)k * f.B) / n_pix);
+#ifdef RS_RAD_AOS  // dev A/B: item-major radiance (rs_kernels.hip put_rad)
+                 const double* rk = L.d_rad + (size_t)3 * (k % f.ring) * f.B;
+#else
                  const double* rk = L.d_rad + (size_t)(k % f.ring) * f.B;
+#endif
                  if (k + 1 < f.n_batches) {
                      HIP_OK(hipStreamWaitEvent(L.acc_stream, done_ev(k), 0));
                      HIP_OK(launch_accumulate(rk, ring_items, L.d_acc, n_pix, planes, k == 0, 0, fp, d_out, nullptr, 0,
@@ -1937,7 +1951,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         path_ms += ms;
     }
     double kernel_ms = 0.0;
-    for (size_t k = 0; k < P.ki; ++k) {
+    for (size_t k = 0; P.timed && k < P.ki; ++k) {  // (a counted, untimed frame has no kernel events)
         float ms = 0;
         HIP_OK(hipEventElapsedTime(&ms, P.kev[2 * k], P.kev[2 * k + 1]));
         kernel_ms += ms;
@@ -2280,6 +2294,7 @@ int rs_scene_create(rs_scene** out) {
         v = s->frames_in_flight; knob("RS_FRAMES", v); s->frames_in_flight = (uint32_t)std::min<unsigned long long>(v, kMaxSlots);
         v = 0; knob("RS_EXT_SPLIT", v); s->ext_split = v != 0;
         v = 0; knob("RS_SPLIT_RUNS", v); s->split_runs = v != 0;
+        v = 0; knob("RS_SHADE_MERGED", v); if (v) s->shade_split = false;
         v = 0; knob("RS_DUMP_ITERS", v); s->dump_iters = v != 0;
 #endif
         *out = s;

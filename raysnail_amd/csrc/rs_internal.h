@@ -166,9 +166,11 @@ hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathPara
 // every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present; cc / inj
 // (device memory): the frame's camera and the iteration's injection (its camera samples are regenerated, not
 // read back); ring: the rad channel stride
+// cam: the iteration injects camera samples (the launch regenerates them); split: the spheres mode's lean and heavy
+// material classes in two launches (k_wfs_shade_all PS)
 hipError_t launch_wfs_shade_all(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
                                 uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
-                                uint64_t ring, double* rad, uint32_t blocks, int sm, hipStream_t st);
+                                uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, int sm, hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
 hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
 hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st);

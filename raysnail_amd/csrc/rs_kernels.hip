@@ -77,9 +77,24 @@ __device__ __forceinline__ T nld(const void* base, uint32_t byte_off) {
     else return gld<T>(base, byte_off);
 }
 
+// A sample's radiance in a rad buffer: channel-major (channel c of item at c * stride + item) or, with
+// RS_RAD_AOS (dev A/B), item-major (3 doubles per item: a scattered end-of-path write touches one line)
+__device__ __forceinline__ void put_rad(double* __restrict__ rad, uint64_t stride, uint64_t item, double r, double g,
+                                        double b) {
+#ifdef RS_RAD_AOS
+    (void)stride;
+    rad[3 * item] = r; rad[3 * item + 1] = g; rad[3 * item + 2] = b;
+#else
+    rad[item] = r; rad[stride + item] = g; rad[2 * stride + item] = b;
+#endif
+}
+
 #ifdef RS_TRAV_STATS  // dev builds only (tools/build_variant.sh -DRS_TRAV_STATS): traversal counters
-__device__ unsigned long long g_trav_stats[32];  // [8 + b]: rays with 8b .. 8b+7 node steps (b < 16, last = more)
-#define RS_STAT(k, v) atomicAdd(&g_trav_stats[k], (unsigned long long)(v))
+// [cat][k], cat 0 camera rays / bounce-synchronous rays, 1 the carried front run (light-sample rays), 2 the rest;
+// [cat][8 + b]: rays with 8b .. 8b+7 node steps (b < 16, last = more). One array per translation unit (each
+// mode's kernels are their own code object): rs_debug_trav_stats_<unit> reads that unit's.
+__device__ unsigned long long g_trav_stats[4][32];
+#define RS_STAT(k, v) atomicAdd(&g_trav_stats[st_cat][k], (unsigned long long)(v))
 __shared__ int s_st_nodes[256], s_st_leaves[256], s_st_witer[256];
 #endif
 
@@ -406,7 +421,7 @@ __device__ __forceinline__ StkT<OVF, N> make_stk(const DScene& S, int* stk_all) 
 #ifdef RS_TRAV_STATS
 // all 64 lanes converged: per ray sums, per wave the max node count (the wave runs the union of its
 // lanes' loops) and the wave's live lanes
-__device__ __forceinline__ void trav_stats_flush(bool live) {
+__device__ __forceinline__ void trav_stats_flush(bool live, int st_cat = 0) {
     int n = live ? s_st_nodes[threadIdx.x] : 0, l = live ? s_st_leaves[threadIdx.x] : 0, mx = n, cnt = live ? 1 : 0;
     for (int off = 32; off > 0; off >>= 1) {
         n += __shfl_xor(n, off, 64); l += __shfl_xor(l, off, 64); cnt += __shfl_xor(cnt, off, 64);
@@ -415,7 +430,7 @@ __device__ __forceinline__ void trav_stats_flush(bool live) {
     int wi = live ? s_st_witer[threadIdx.x] : 0;  // the wave's leaf-loop passes: the max over its lanes
     for (int off = 32; off > 0; off >>= 1) wi = max(wi, __shfl_xor(wi, off, 64));
     if ((threadIdx.x & 63) == 0 && cnt) { RS_STAT(0, n); RS_STAT(1, l); RS_STAT(2, cnt); RS_STAT(3, mx); RS_STAT(4, cnt); RS_STAT(5, 1); RS_STAT(6, wi); }
-    if (live) RS_STAT(8 + min(15, s_st_nodes[threadIdx.x] / 8), 1);
+    if (live) RS_STAT(8 + min(15, max(0, s_st_nodes[threadIdx.x]) / 8), 1);
 }
 #endif
 // One node of the 4-wide near-first traversal: test the four child boxes of one 128-byte node,
@@ -588,7 +603,7 @@ __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, flo
 // World::hit of a flat scene with a 4-wide tree through queued leaf passes (above). q: this lane's
 // column of the block's FIFO array (RS_LEAFQ x kBlock ints). Every lane of the wave that calls it
 // must call it (the pass choice is a ballot over the calling lanes).
-template <int SM, class STK>
+template <int SM, class STK, bool TOUT = false>
 __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk,
                                                int* q) {
     const RayC rc = ray_consts(r);
@@ -632,7 +647,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
     s_st_leaves[threadIdx.x] = st_leaves;
     s_st_witer[threadIdx.x] = st_witer;
 #endif
-    bend_out = bend;
+    bend_out = TOUT ? best : bend;
     return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
@@ -655,6 +670,9 @@ __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, 
     double best = RS_INF, bend = RS_INF;
     int bp = -1;
     uint32_t skip = 0;
+#ifdef RS_TRAV_STATS
+    int st_nodes = 0, st_leaves = 0;
+#endif
     while (true) {
         uint32_t found = 0;  // leaves met by this walk; slots skip .. skip + K - 1 are listed
         {
@@ -675,6 +693,9 @@ __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, 
                 const float hi[3] = {nld<true, float>(S.nodes4, nb + 48u), nld<true, float>(S.nodes4, nb + 64u),
                                      nld<true, float>(S.nodes4, nb + 80u)};
                 float e;
+#ifdef RS_TRAV_STATS
+                ++st_nodes;  // (deferred walk: box tests)
+#endif
                 if (slab32(lo, hi, rf, tmin32, __builtin_huge_valf(), e)) {
                     if (c < 0) {
                         if (found >= skip && found - skip < K) q[(found - skip) * kBlock] = c;
@@ -695,9 +716,17 @@ __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, 
         }
         const uint32_t m = found > skip ? min(found - skip, K) : 0u;
         for (uint32_t i = 0; i < m; ++i) test_leaf<SM, true>(S, ~q[i * kBlock], r, rc, tmin, best, bend, bp);
+#ifdef RS_TRAV_STATS
+        st_leaves += (int)m;
+#endif
         if (found <= skip + K) break;
         skip += K;
     }
+#ifdef RS_TRAV_STATS
+    s_st_nodes[threadIdx.x] = st_nodes;
+    s_st_leaves[threadIdx.x] = st_leaves;
+    s_st_witer[threadIdx.x] = 0;
+#endif
     bend_out = bend;
     return bp;  // nest modes' leaf codes name prims (no lprim)
 }
@@ -705,12 +734,18 @@ __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, 
 // World::hit, inlined into the kernels of every scene mode (a real call makes the kernel keep its live
 // registers in scratch across it: the nest-2 extend spilled 1.2 KB per lane; the generic mode as a
 // call measured slower in round 3, profiles/r3/ab/generic_inline_*.txt)
-template <int SM, class STK, bool LOBJ = false>
+// TOUT: bend_out receives the winner's own t (best) instead of the range end it was accepted under (the spheres
+// mode's shading rebuilds the record from t: sphere_rec_at)
+template <int SM, class STK, bool LOBJ = false, bool TOUT = false>
 __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if (S.root < 0) return -1;
     // nest-0 only: on nest-2 (C4's scene) the split walk measured 2 % slower, on nest-0 (example.sdl)
     // 2.5 % faster (profiles/r4/ab/deferred_leaves)
+#ifdef RS_NEST2_DEFER  // dev A/B: nest-2 scenes with an LDS image walk with deferred leaf tests too
+    if constexpr (LOBJ && (SM == kSmNest0 || SM == kSmNest2)) return traverse_deferred<SM>(S, r, tmin, bend_out, stk);
+#else
     if constexpr (LOBJ && SM == kSmNest0) return traverse_deferred<SM>(S, r, tmin, bend_out, stk);
+#endif
     const RayC rc = ray_consts(r);
     const RayF rf = make_rayf(r.o, rc.inv);
     const float tmin32 = -round_up_f(-tmin);
@@ -817,7 +852,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
     s_st_leaves[threadIdx.x] = st_leaves;
     s_st_witer[threadIdx.x] = st_witer;
 #endif
-    bend_out = bend;
+    bend_out = TOUT ? best : bend;
     return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
@@ -1058,9 +1093,7 @@ __global__ __launch_bounds__(kBlock) void k_path_mega(const DScene* __restrict__
             Ray r = camera_ray(C, u, v, rng);
             L = trace_path<SM>(S, r, P.depth, rng, stk, segs);
         }
-        rad[item] = L.x;
-        rad[P.n_items + item] = L.y;
-        rad[2 * P.n_items + item] = L.z;
+        put_rad(rad, P.n_items, item, L.x, L.y, L.z);
     }
     // wave-reduce the segment count, one atomic per wave, spread over 256 counters
     unsigned long long s64 = segs;
@@ -1152,6 +1185,38 @@ __device__ __forceinline__ uint32_t block_slot(int cls, uint32_t* const* counter
     uint32_t slot = 0;
     if (cls >= 0 && cls < C) slot = bbase[cls] + wcnt[cls][wave] + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull));
     __syncthreads();  // wcnt / bbase are reused by the next call
+    return slot;
+}
+// block_slot for C runs whose lanes are also ordered by a key in [0, K) inside the block's chunk of each run:
+// slots of run c are the run's block base + (key, wave, lane) order, so consecutive records of a run hold
+// rays of one key (one atomic per block and run, as block_slot).
+template <int C, int K>
+__device__ __forceinline__ uint32_t block_slot_keyed(int cls, int key, uint32_t* const* counters) {
+    __shared__ uint32_t wk[C][K][kBlock / 64];
+    __shared__ uint32_t kb[C];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long mine = 0ull;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const bool me = cls == c && key == k;
+            const unsigned long long m = __ballot(me);
+            if (me) mine = m;
+            if (lane == 0) wk[c][k][wave] = (uint32_t)__popcll(m);
+        }
+    __syncthreads();
+    if (threadIdx.x < C) {
+        const int c = threadIdx.x;
+        uint32_t tot = 0;
+        for (int k = 0; k < K; ++k)
+            for (int w = 0; w < kBlock / 64; ++w) { const uint32_t n = wk[c][k][w]; wk[c][k][w] = tot; tot += n; }
+        kb[c] = tot ? atomicAdd(counters[c], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t slot = 0;
+    if (cls >= 0 && cls < C) slot = kb[cls] + wk[cls][key][wave] + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull));
+    __syncthreads();
     return slot;
 }
 __device__ __forceinline__ uint32_t block_slot1(bool flag, uint32_t* counter) {
@@ -1253,7 +1318,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
     if (i < n) {
         item = item0 + gen_perm(i, item0, n, P);
         live = camera_sample(C, P, item, r, rng);
-        if (!live) { rad[item] = 0.0; rad[P.n_items + item] = 0.0; rad[2 * P.n_items + item] = 0.0; }
+        if (!live) put_rad(rad, P.n_items, item, 0.0, 0.0, 0.0);
     }
     if (!P.mask && P.depth > 0) {
         // no pixel mask: every camera sample is live, so record i is thread i's (no compaction, and
@@ -1324,7 +1389,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ 
                 L = close_path(L, T);
                 alive = false;
             }
-            if (!alive) { rad[item] = L.x; rad[n_items + item] = L.y; rad[2 * n_items + item] = L.z; }
+            if (!alive) put_rad(rad, n_items, item, L.x, L.y, L.z);
         }
         const uint32_t slot = block_slot1(alive, &W.counts[bounce + 1]);
         if (alive) store_path(nxt, slot, r, T, rng, item);
@@ -1356,7 +1421,13 @@ constexpr int kClsLight = 6;
 // 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 with the LDS image 3 (168 VGPRs, 184 B
 // of scratch: 4 % faster than 2 waves, 4 waves 12 % slower; profiles/r4/ab/nest2_registers), nest-2
 // with its tables in global memory 2 (its loads are L1 / L2 round trips that the spills would join)
-constexpr int ext_min_waves(int sm, bool lobj = false) { return sm == kSmNest2 ? (lobj ? 3 : 2) : 4; }
+constexpr int ext_min_waves(int sm, bool lobj = false, int part = kExtAll) {
+#ifdef RS_EXT_W5  // dev A/B: the spheres mode's carried-path extend at 5 waves (96 VGPRs, 12 B of scratch)
+    if (sm == kSmSpheres && part == kExtCarried) return 5;
+#endif
+    (void)part;
+    return sm == kSmNest2 ? (lobj ? 3 : 2) : 4;
+}
 
 // The scene's LDS image (DScene::limg, nest modes): the block copies it into its dynamic LDS and
 // reads the tree and the object tables through a DScene copy whose table pointers point there.
@@ -1395,7 +1466,7 @@ __device__ __forceinline__ void lds_scene(const DScene* __restrict__ Sp, DScene&
 // against two waves for each part)
 // LOBJ: the scene's tables from its LDS image (lds_scene; the launch passes limg_bytes of dynamic LDS)
 template <int SM, bool OVF, int PART, bool LOBJ>
-__global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W,
+__global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W,
                                                                           uint32_t* const* __restrict__ queues, uint32_t it,
                                                                           double* __restrict__ rad, DCamera C, PathParams P,
                                                                           InjParams I) {
@@ -1404,6 +1475,9 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
     const DScene& S = LOBJ ? Sv : *Sp;  // otherwise the scene in device memory (no by-value copy in scratch)
     __shared__ int stk_all[stack_lds(SM) * kBlock];
     const StkT<OVF, stack_lds(SM)> stk = make_stk<OVF, stack_lds(SM)>(S, stk_all);
+#ifdef RS_SPH_LEAFQ
+    __shared__ int leafq[SM == kSmSpheres ? RS_LEAFQ * kBlock : 1];
+#endif
     uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
     const uint32_t nf = cnt[cix(kCntFront)];
     const uint32_t n_old = PART == kExtCamera ? 0u : nf + cnt[cix(kCntBack)];
@@ -1430,7 +1504,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
                 uint64_t g;
                 inj_sample(I, P, j - n_old, g, item);
                 live = camera_sample(C, P, g, r, rng);
-                if (!live) { rad[item] = 0.0; rad[I.ring + item] = 0.0; rad[2 * I.ring + item] = 0.0; }
+                if (!live) put_rad(rad, I.ring, item, 0.0, 0.0, 0.0);
             } else {
                 r = load_ray(cur, i);
                 live = true;
@@ -1442,7 +1516,17 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
             if (base == base0) lds_fill(S);
         if (live) {
             double bend = RS_INF;
-            const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ>(S, r, 0.0001, bend, stk);
+            // the spheres mode keeps the winner's t (W.hit: the shading's sphere_rec_at), the others the range end
+            constexpr bool kT = SM == kSmSpheres;
+#ifdef RS_SPH_LEAFQ  // dev A/B: the spheres mode's leaves through the per-lane leaf FIFO (traverse_flat_q)
+            int bp;
+            if constexpr (SM == kSmSpheres)
+                bp = traverse_flat_q<SM, StkT<OVF, stack_lds(SM)>, true>(S, r, 0.0001, bend, stk, leafq + threadIdx.x);
+            else
+                bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ, kT>(S, r, 0.0001, bend, stk);
+#else
+            const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ, kT>(S, r, 0.0001, bend, stk);
+#endif
             V3 add;
             bool done = true;
             if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
@@ -1454,7 +1538,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
                     int mi;
                     if (SM == kSmSpheres) {
                         const DPrim Pr = S.prims[bp];
-                        sphere_hit(S.spheres[Pr.idx], Pr.mat, r, 0.0001, bend, h);
+                        sphere_rec_at(S.spheres[Pr.idx], Pr.mat, r, bend, h);  // bend: the winner's t (kT)
                         mi = Pr.mat;
                     } else {
                         // emission reads the record's material and point only: for a leaf object
@@ -1489,13 +1573,15 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
                 } else {
                     t4 = cur.thr[i]; item = cur.tag[i].x;
                 }
-                rad[item] = 0.0 + t4.x * add.x;
-                rad[I.ring + item] = 0.0 + t4.y * add.y;
-                rad[2 * I.ring + item] = 0.0 + t4.z * add.z;
+                put_rad(rad, I.ring, item, 0.0 + t4.x * add.x, 0.0 + t4.y * add.y, 0.0 + t4.z * add.z);
             }
         }
 #ifdef RS_TRAV_STATS
-        trav_stats_flush(live);
+        {   // the wave's category: its first live lane's
+            const int c = gen ? 0 : j < nf ? 1 : 2;
+            const unsigned long long lm = __ballot(live);
+            trav_stats_flush(live, lm ? __shfl(c, __ffsll((long long)lm) - 1, 64) : 0);
+        }
 #endif
         // the iteration's live camera samples are counted in the same block reduction (the carried
         // paths are cnt[0]), on one of kStatLines counters by block (one atomic per block on a single
@@ -1511,11 +1597,12 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ)) void k_wfs_extend(
 // One batch of 256 queued paths of material class KIND (-1: the generic material switch; entries
 // base .. base + 255 of a queue of n): finish the hit record, scatter, write the radiance of paths that
 // end and append the survivors to the next set. Must be called by every thread of the block (block_slot).
-// Camera samples injected by the iteration (records nf .. nf + I.n_new - 1 of the set, nf = its front run)
-// have no record: the extend traced them from registers, and here they are regenerated from their slot
-// (inj_sample + camera_sample: the same ray and RNG state, T = 1, level 0) instead of being written and
-// read back (104 B each way per camera sample that reaches a surface).
-template <int KIND, int SM>
+// CAM (launches of iterations that inject camera samples): the injected samples (records nf .. nf + n_new - 1
+// of the set, nf = its front run) have no record -- the extend traced them from registers -- and are
+// regenerated here from their slot (inj_sample + camera_sample: the same ray and RNG state, T = 1, level 0)
+// instead of being written and read back (104 B each way per camera sample that reaches a surface). Launches
+// of iterations without injections compile none of it (the regeneration's registers spilled in them).
+template <int KIND, int SM, bool CAM>
 __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const uint32_t* __restrict__ queue,
                                                 uint32_t n, uint32_t base, uint32_t it, uint32_t nf, uint32_t* cnt_next,
                                                 uint32_t depth, uint64_t ring, double* __restrict__ rad,
@@ -1533,19 +1620,11 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     if (j < n) {
         const uint32_t i = queue[j];
         const uint32_t jg = i - nf;
-#if defined(RS_CAM_RECORDS)
-        if (false) {
-#elif defined(RS_CAM_FAKE)  // dev bound: no record read and no regeneration (wrong frames)
-        if (jg < n_new) {
-            item = jg; r.o = v3((double)i, 1.0, 2.0); r.d = v3(0.0, 1.0, 0.0); r.time = 0.0; rng.x = rng.y = rng.z = rng.w = jg | 1u;
-            T = v3(1.0, 1.0, 1.0);
-#else
-        if (jg < n_new) {
+        if (CAM && jg < n_new) {
             uint64_t g;
             inj_sample(*inj, cc->P, jg, g, item);
             camera_sample_xy_item(cc->C, cc->P, g, r, rng);
             T = v3(1.0, 1.0, 1.0);
-#endif
         } else {
             load_path(cur, i, r, T, rng);
             const uint2 tg = cur.tag[i];
@@ -1555,7 +1634,12 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
         const double2 hb = W.hit[i];
         const int bp = (int)__double_as_longlong(hb.x);
         Hit h;
-        finish_hit<SM, (KIND >= 0)>(S, bp, r, 0.0001, hb.y, h);
+        if constexpr (SM == kSmSpheres) {  // hb.y: the winner's t (k_wfs_extend kT)
+            const DPrim P = S.prims[bp];
+            sphere_rec_at(S.spheres[P.idx], P.mat, r, hb.y, h);
+        } else {
+            finish_hit<SM, (KIND >= 0)>(S, bp, r, 0.0001, hb.y, h);
+        }
         const int mi = h.mat >= 0 ? h.mat : S.default_mat;
         const DMaterial& M0 = S.mats[mi];
         bool cont;
@@ -1566,7 +1650,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
             // None (camera.rs:172-176, 250), 0 + T * e as in shade_step
             const V3 e = emission<0>(S, M0, h);
             const V3 L = v3(0.0, 0.0, 0.0) + v3(T.x * e.x, T.y * e.y, T.z * e.z);
-            rad[item] = L.x; rad[ring + item] = L.y; rad[2 * ring + item] = L.z;
+            put_rad(rad, ring, item, L.x, L.y, L.z);
             cont = false;
             item = ~0u;  // radiance written
         } else {
@@ -1580,13 +1664,18 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
         alive = cont && (lvl + 1 < depth);  // the depth limit of ray_color (camera.rs:161)
         if (!alive && item != ~0u) {  // absorbed or depth limit: no emission term
             const V3 L = close_path(v3(0.0, 0.0, 0.0), T);
-            rad[item] = L.x; rad[ring + item] = L.y; rad[2 * ring + item] = L.z;
+            put_rad(rad, ring, item, L.x, L.y, L.z);
         }
     }
     // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
     // the front, the rest from the back: the next extend's waves then trace rays of one kind
     uint32_t* const gc[2] = {&cnt_next[cix(kCntBack)], &cnt_next[cix(kCntFront)]};
+#ifdef RS_BIN_OCT  // dev A/B: the next set's runs ordered by direction octant inside each block's chunk
+    const int oct = (r.d.x < 0.0 ? 1 : 0) | (r.d.y < 0.0 ? 2 : 0) | (r.d.z < 0.0 ? 4 : 0);
+    const uint32_t slot = block_slot_keyed<2, 8>(alive ? light_ray : -1, oct, gc);
+#else
     const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
+#endif
     if (alive) {
         const uint32_t p = light_ray ? slot : W.cap - 1u - slot;
         store_path(nxt, p, r, T, rng, item, lvl + 1u);
@@ -1601,8 +1690,10 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // then (it sets the kernel's register count). LOBJ: the scene's tables from its LDS image (lds_scene).
 // Waves: 3; nest-2 with class 4 and the tables in global memory 1 (bounded to 3 it spilled and lost
 // 21 % on C4 in round 3; with the LDS image 3 waves measured 5 % faster than 2: nest2_registers)
-template <int SM, bool G4, bool LOBJ>
-__global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
+// PS: the classes of this launch -- 0 all; 1 the lean ones (Lambertian, Metal, Dielectric: bounded to 4 waves);
+// 2 the heavy ones (DiffuseMetal's two ONBs and ReflectionPdf loop, the generic switch) -- RS_SHADE_SPLIT
+template <int SM, bool G4, bool LOBJ, int PS, bool CAM>
+__global__ __launch_bounds__(kBlock, PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
@@ -1618,11 +1709,12 @@ __global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) vo
     const uint32_t nf = cnt[cix(kCntFront)];  // the front run: the injected camera samples' slots follow it
     const uint32_t n_new = inj->n_new;
     constexpr int NC = G4 ? 5 : 4;
+    constexpr uint32_t kPart = PS == 0 ? 0x1fu : PS == 1 ? 0x0bu : 0x14u;  // classes of this launch
     uint32_t n[NC], first[NC + 1];
     first[0] = 0;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-        n[k] = (class_mask >> k & 1u) ? cnt[cix(1 + k)] : 0u;
+        n[k] = ((class_mask & kPart) >> k & 1u) ? cnt[cix(1 + k)] : 0u;
         first[k + 1] = first[k] + (n[k] + kBlock - 1) / kBlock;
     }
     for (uint32_t v = blockIdx.x; v < first[NC]; v += gridDim.x) {
@@ -1630,16 +1722,22 @@ __global__ __launch_bounds__(kBlock, (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) vo
 #pragma unroll
         for (int c = 1; c < NC; ++c) k += v >= first[c] ? 1 : 0;
         const uint32_t base = (v - first[k]) * kBlock;
-        if (k == 0)
-            wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], n[0], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
-        else if (k == 1)
-            wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], n[1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
-        else if (k == 2)
-            wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], n[2], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
-        else if (k == 3 || !G4)
-            wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], n[3], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
-        else
-            wfs_shade_batch<-1, SM>(S, W, queues[NC - 1], n[NC - 1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+        if (k == 0) {
+            if constexpr ((kPart & 1u) != 0)
+                wfs_shade_batch<RS_MAT_LAMBERTIAN, SM, CAM>(S, W, queues[0], n[0], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+        } else if (k == 1) {
+            if constexpr ((kPart & 2u) != 0)
+                wfs_shade_batch<RS_MAT_METAL, SM, CAM>(S, W, queues[1], n[1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+        } else if (k == 2) {
+            if constexpr ((kPart & 4u) != 0)
+                wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM, CAM>(S, W, queues[2], n[2], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+        } else if (k == 3 || !G4) {
+            if constexpr ((kPart & 8u) != 0)
+                wfs_shade_batch<RS_MAT_DIELECTRIC, SM, CAM>(S, W, queues[3], n[3], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+        } else {
+            if constexpr ((kPart & 16u) != 0)
+                wfs_shade_batch<-1, SM, CAM>(S, W, queues[NC - 1], n[NC - 1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+        }
     }
 }
 
@@ -1657,18 +1755,29 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict_
     // (rs_host.cpp counts_clean; the host passes n_zero = 0 when it still reads them)
     for (uint64_t z = t; z < n_zero; z += (uint64_t)gridDim.x * kBlock) zero[z] = 0u;
     if (t >= 3ull * n_pix) return;
+#ifdef RS_RAD_AOS  // item-major radiance: thread 3p + c, so a wave's reads of a sample plane are contiguous
+    const uint32_t p = (uint32_t)(t / 3), c = (uint32_t)(t - 3ull * p);
+#else
     const uint32_t c = (uint32_t)(t / n_pix), p = (uint32_t)(t - (uint64_t)c * n_pix);
+#endif
     double a = first ? 0.0 : acc[(uint64_t)c * n_pix + p];
+#ifdef RS_RAD_AOS
+    const double* rc = rad + 3ull * p + c;
+    const uint64_t sstep = 3ull * n_pix;
+    (void)stride;
+#else
     const double* rc = rad + (uint64_t)c * stride + p;
+    const uint64_t sstep = n_pix;
+#endif
     uint32_t s = 0;
     for (; s + 16 <= n_samp; s += 16) {
         double v[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = rc[(uint64_t)(s + k) * n_pix];
+        for (int k = 0; k < 16; ++k) v[k] = rc[(uint64_t)(s + k) * sstep];
 #pragma unroll
         for (int k = 0; k < 16; ++k) a = a + v[k];
     }
-    for (; s < n_samp; ++s) a = a + rc[(uint64_t)s * n_pix];
+    for (; s < n_samp; ++s) a = a + rc[(uint64_t)s * sstep];
     if (!last) {
         acc[(uint64_t)c * n_pix + p] = a;
         return;
@@ -1825,8 +1934,8 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
       (s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1))                                                  \
     X(hipError_t, wfs_shade_all, (const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w, \
                                   uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,      \
-                                  uint64_t ring, double* rad, uint32_t blocks, hipStream_t st),                   \
-      (s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks, st))
+                                  uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, hipStream_t st), \
+      (s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks, cam, split, st))
 #define RS_DECLARE_SM(R, NAME, PARAMS, ARGS) template <int SMC> R NAME##_sm PARAMS;
 RS_SM_LAUNCHERS(RS_DECLARE_SM)
 RS_SORTED_LAUNCHERS(RS_DECLARE_SM)
@@ -1912,18 +2021,32 @@ hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& 
 template <int SMC>
 hipError_t wfs_shade_all_sm(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
                             uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
-                            uint64_t ring, double* rad, uint32_t blocks, hipStream_t st) {
+                            uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, hipStream_t st) {
     if (!blocks) return hipSuccess;
-#define RS_SHADE_LAUNCH(G4, LOBJ, SHM)                                                                              \
-    hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, queues, class_mask, \
-                       it, depth, ring, rad, cc, inj)
+#define RS_SHADE_LAUNCH(G4, LOBJ, PS, SHM)                                                                          \
+    do {                                                                                                        \
+        if (cam)                                                                                                \
+            hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ, PS, true>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, \
+                               queues, class_mask, it, depth, ring, rad, cc, inj);                             \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ, PS, false>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, \
+                               queues, class_mask, it, depth, ring, rad, cc, inj);                             \
+    } while (0)
     const uint32_t shm = s.host->limg_bytes;  // nest modes' LDS image (none in the spheres mode)
     if constexpr (SMC == kSmNest0 || SMC == kSmNest2) {
-        if (class_mask & (1u << 4)) { if (shm) RS_SHADE_LAUNCH(true, true, shm); else RS_SHADE_LAUNCH(true, false, 0); }
-        else { if (shm) RS_SHADE_LAUNCH(false, true, shm); else RS_SHADE_LAUNCH(false, false, 0); }
+        if (class_mask & (1u << 4)) { if (shm) RS_SHADE_LAUNCH(true, true, 0, shm); else RS_SHADE_LAUNCH(true, false, 0, 0); }
+        else { if (shm) RS_SHADE_LAUNCH(false, true, 0, shm); else RS_SHADE_LAUNCH(false, false, 0, 0); }
+    } else if (split) {
+        // the lean classes (Lambertian, Metal, Dielectric) at 4 waves, then the heavy ones (DiffuseMetal, the
+        // generic switch) at 3: the merged kernel's registers are DiffuseMetal's (168), Lambertian alone 133
+        RS_SHADE_LAUNCH(false, false, 1, 0);
+        if (class_mask & 0x14u) {
+            if (class_mask & (1u << 4)) RS_SHADE_LAUNCH(true, false, 2, 0);
+            else RS_SHADE_LAUNCH(false, false, 2, 0);
+        }
     } else {
-        if (class_mask & (1u << 4)) RS_SHADE_LAUNCH(true, false, 0);
-        else RS_SHADE_LAUNCH(false, false, 0);
+        if (class_mask & (1u << 4)) RS_SHADE_LAUNCH(true, false, 0, 0);
+        else RS_SHADE_LAUNCH(false, false, 0, 0);
     }
 #undef RS_SHADE_LAUNCH
     return hipGetLastError();
@@ -1986,8 +2109,9 @@ hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathPara
 
 hipError_t launch_wfs_shade_all(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
                                 uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
-                                uint64_t ring, double* rad, uint32_t blocks, int sm, hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks, st));
+                                uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, int sm, hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks,
+                                                           cam, split, st));
     return hipErrorInvalidValue;
 }
 
@@ -2037,11 +2161,26 @@ hipError_t launch_finalize(const double* acc, float* out_rgba, const FinalParams
 
 }  // namespace rs
 
-#if defined(RS_TRAV_STATS) && RS_TU_COMMON
-extern "C" int rs_debug_trav_stats(unsigned long long out[32], int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rs::g_trav_stats), 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
+#if defined(RS_TRAV_STATS)
+#if !defined(RS_TU)
+#define RS_TS_FN rs_debug_trav_stats
+#elif RS_TU < 0
+#define RS_TS_FN rs_debug_trav_stats_c
+#elif RS_TU == 0
+#define RS_TS_FN rs_debug_trav_stats_0
+#elif RS_TU == 1
+#define RS_TS_FN rs_debug_trav_stats_1
+#elif RS_TU == 2
+#define RS_TS_FN rs_debug_trav_stats_2
+#elif RS_TU == 3
+#define RS_TS_FN rs_debug_trav_stats_3
+#else
+#define RS_TS_FN rs_debug_trav_stats_4
+#endif
+extern "C" int RS_TS_FN(unsigned long long out[128], int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rs::g_trav_stats), 128 * sizeof(unsigned long long)) != hipSuccess) return -3;
     if (reset) {
-        unsigned long long z[32] = {0};
+        unsigned long long z[128] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(rs::g_trav_stats), z, sizeof(z)) != hipSuccess) return -3;
     }
     return 0;
