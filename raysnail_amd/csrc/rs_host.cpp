@@ -182,10 +182,6 @@ struct Slot {
     size_t counts_clean = 0;  // leading entries of d_counts known to be zero (reset by the last frame's accumulate)
     hipStream_t acc_stream = nullptr;         // streaming wavefront: the batches' accumulates
     std::vector<hipEvent_t> bev;              // per batch: its paths done, its accumulate done
-    // streaming wavefront: the frame's CamConsts + every iteration's InjParams (device copy, pinned staging,
-    // the event of the last upload: the staging is rewritten only once that copy has run)
-    void* d_fc = nullptr; void* h_fc = nullptr; size_t fc_cap = 0;
-    hipEvent_t fc_ev = nullptr; bool fc_rec = false;
 
     // wait until nothing in flight uses this slot's buffers
     void quiesce() {
@@ -193,18 +189,14 @@ struct Slot {
             if (lane[l]) HIP_OK(hipStreamSynchronize(lane[l]));
         if (acc_stream) HIP_OK(hipStreamSynchronize(acc_stream));
         if (free_rec) HIP_OK(hipEventSynchronize(free_ev));
-        if (fc_rec) HIP_OK(hipEventSynchronize(fc_ev));
     }
     void release() {
         for (uint32_t l = 0; l < kMaxLanes; ++l)
             if (lane[l]) (void)hipStreamSynchronize(lane[l]);
         if (acc_stream) (void)hipStreamSynchronize(acc_stream);
         if (free_rec) (void)hipEventSynchronize(free_ev);
-        if (fc_rec) (void)hipEventSynchronize(fc_ev);
-        for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts, d_fc})
+        for (void* p : {(void*)d_rad, (void*)d_acc, (void*)d_cnt, (void*)d_mask, (void*)d_out, d_wf, (void*)d_counts})
             if (p) (void)hipFree(p);
-        if (h_fc) (void)hipHostFree(h_fc);
-        if (fc_ev) (void)hipEventDestroy(fc_ev);
         for (uint32_t l = 0; l < kMaxLanes; ++l) {
             if (lane[l]) (void)hipStreamDestroy(lane[l]);
             if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
@@ -227,6 +219,7 @@ struct Replica {
     Slot slots[kMaxSlots];
     uint32_t next_slot = 0;
     int n_cu = 0, ext_bpc = 0, shade_bpc = 0;
+    uint64_t mem_total = 0;                 // device memory (bytes): caps the streaming pool (pool_limit)
     int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond the LDS part)
     DScene* d_ds = nullptr;                 // ds in device memory (what the kernels read)
     DScene uploaded{};                      // the copy last written to d_ds
@@ -276,7 +269,11 @@ struct rs_scene {
     // workspace (rs_scene_set_workspace): camera samples per rad batch buffer; paths per set of the
     // streaming pool / per chunk of the bounce-synchronous wavefront
     uint64_t max_items_per_batch = 32ull << 20;
-    uint64_t pool_paths = 64ull << 20;
+    // streaming pool bound (paths per set): a frame injects Q samples per iteration with Q * min(depth, iterations)
+    // <= the pool, so a larger pool means fewer, fuller iterations on big depth-50 frames (C3 1920x1080x256:
+    // 64 Mi 210.9 ms, 128 Mi 197.1 ms, 256 Mi 190.7 ms; profiles/r5/ab/pool_sizes_r5c.jsonl); each replica caps it
+    // by its device memory (Replica::pool_limit)
+    uint64_t pool_paths = 256ull << 20;
     uint32_t inject_div = 1;                      // streaming: inject up to 1/inject_div of a lane per iteration
     uint32_t wf_lanes = 2;                        // chunk lanes of the bounce-synchronous wavefront (rs_scene_set_lanes)
     uint32_t stream_lanes = 1;                    // lanes of the streaming wavefront (rs_scene_set_lanes)
@@ -804,6 +801,7 @@ void upload_replica(rs_scene* s, int device) {
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
     R->n_cu = prop.multiProcessorCount;
+    R->mem_total = (uint64_t)prop.totalGlobalMem;
     HIP_OK(wf_occupancy(s->scene_mode, &R->ext_bpc, &R->shade_bpc));
     s->reps.push_back(std::move(R));
 }
@@ -1427,7 +1425,7 @@ void walk(const FrameSched& f, FI visit, FA acc) {
         }
     }
 }
-FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D, uint32_t want_lanes) {
+FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D, uint32_t want_lanes, uint64_t pool) {
     FrameSched f;
     // batches: at most max_items_per_batch items, and at least one per lane
     uint32_t spb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(N, s->max_items_per_batch / n_pix));
@@ -1452,7 +1450,7 @@ FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D,
         const uint64_t Dm = std::max<uint32_t>(D, 1);
         uint64_t q = std::min<uint64_t>(f.B, std::max<uint64_t>(kBlock, (L.total + s->inject_div - 1) / s->inject_div));
         auto bound = [&](uint64_t qq) { return qq * std::min<uint64_t>(Dm, (L.total + qq - 1) / qq); };
-        if (bound(q) > s->pool_paths) q = std::min<uint64_t>(f.B, std::max<uint64_t>(kBlock, s->pool_paths / Dm));
+        if (bound(q) > pool) q = std::min<uint64_t>(f.B, std::max<uint64_t>(kBlock, pool / Dm));
         L.Q = q;
         L.T_inj = (L.total + q - 1) / q;
         L.T = L.T_inj + (D ? D - 1 : 0);
@@ -1509,6 +1507,18 @@ struct Pending {
     }
 };
 
+// The streaming pool of a frame on replica R: the scene's bound, capped so that the pools of all its frame slots
+// take at most half the device memory (a path's bytes, carve_wf: two sets of 3 x 32 B records + the tag, the hit,
+// a queue slot per class; 288 GB holds two slots of 256 Mi paths)
+uint32_t frame_slots(const rs_scene* s);
+uint64_t pool_limit(const rs_scene* s, const Replica& R) {
+    const uint64_t per_path = 2 * (3 * sizeof(D4) + sizeof(uint2)) + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
+    return std::min<uint64_t>(s->pool_paths, std::max<uint64_t>(kBlock, R.mem_total / 2 / (frame_slots(s) * per_path)));
+}
+
+// samples of a frame from which the spheres mode shades in two launches (rs_scene::shade_split)
+constexpr uint64_t kSplitShadeMin = 8ull << 20;
+
 // Frame slots a replica cycles through (render_enqueue takes slot next_slot % frame_slots): one for trees
 // whose traversal stack spills to the replica's shared HBM overflow array, else frames_in_flight. Callers
 // that keep several frames (bands) in flight must not exceed it: two frames in one slot share its counters.
@@ -1535,8 +1545,7 @@ hipStream_t lane_stream(Slot& L, uint32_t l) {
     return L.lane[l];
 }
 
-// The camera samples lane ln injects at iteration t (InjParams): the frame's enqueue and the shading's
-// regeneration of camera samples (CamConsts upload) use the same values.
+// The camera samples lane ln injects at iteration t (InjParams).
 InjParams inj_params(const FrameSched& f, const LaneSched& ln, uint64_t t, uint64_t ring_items) {
     InjParams I{};
     I.n_new = ln.n_new(t);
@@ -1640,7 +1649,8 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         join_to_S();
         HIP_OK(launch_finalize(L.d_acc, d_out, fp, S));
     } else if (streaming) {
-        const FrameSched f = make_sched(s, n_pix, N, D, ext_spill ? 1u : std::min<uint32_t>(kMaxLanes, s->stream_lanes));
+        const FrameSched f = make_sched(s, n_pix, N, D, ext_spill ? 1u : std::min<uint32_t>(kMaxLanes, s->stream_lanes),
+                                        pool_limit(s, R));
         ensure(L, L.d_rad, L.rad_cap, (size_t)3 * f.ring * f.B);
         carve_wf(L, f.cap, f.lanes);
         n_counts = f.n_counts;
@@ -1655,36 +1665,6 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         if (!L.acc_stream) HIP_OK(hipStreamCreateWithFlags(&L.acc_stream, hipStreamNonBlocking));
         if (!L.fork_ev) HIP_OK(hipEventCreateWithFlags(&L.fork_ev, hipEventDisableTiming));
         const uint64_t ring_items = (uint64_t)f.ring * f.B;
-        // the frame's CamConsts and every iteration's InjParams for the shading (one upload on L0, before the fork)
-        std::vector<size_t> it_off(f.lanes, 0);
-        size_t n_it = 0;
-        for (uint32_t l = 0; l < f.lanes; ++l) { it_off[l] = n_it; n_it += f.lane[l].T; }
-        const size_t fc_head = (sizeof(CamConsts) + 63) & ~(size_t)63;
-        const size_t fc_bytes = fc_head + n_it * sizeof(InjParams);
-        if (fc_bytes > L.fc_cap) {
-            L.quiesce();
-            if (L.d_fc) HIP_OK(hipFree(L.d_fc));
-            if (L.h_fc) HIP_OK(hipHostFree(L.h_fc));
-            L.d_fc = L.h_fc = nullptr;
-            L.fc_cap = 0;
-            HIP_OK(hipMalloc(&L.d_fc, fc_bytes));
-            HIP_OK(hipHostMalloc(&L.h_fc, fc_bytes, hipHostMallocDefault));
-            L.fc_cap = fc_bytes;
-        }
-        if (!L.fc_ev) HIP_OK(hipEventCreateWithFlags(&L.fc_ev, hipEventDisableTiming));
-        if (L.fc_rec) HIP_OK(hipEventSynchronize(L.fc_ev));  // the staging's previous upload has run
-        {
-            CamConsts cc{dc, pp};
-            std::memcpy(L.h_fc, &cc, sizeof(cc));
-            InjParams* hi = (InjParams*)((char*)L.h_fc + fc_head);
-            for (uint32_t l = 0; l < f.lanes; ++l)
-                for (uint64_t t = 0; t < f.lane[l].T; ++t) hi[it_off[l] + t] = inj_params(f, f.lane[l], t, ring_items);
-        }
-        HIP_OK(hipMemcpyAsync(L.d_fc, L.h_fc, fc_bytes, hipMemcpyHostToDevice, L0));
-        HIP_OK(hipEventRecord(L.fc_ev, L0));
-        L.fc_rec = true;
-        const CamConsts* d_cc = (const CamConsts*)L.d_fc;
-        const InjParams* d_inj = (const InjParams*)((const char*)L.d_fc + fc_head);
         HIP_OK(hipEventRecord(L.fork_ev, L0));
         for (uint32_t l = 1; l < f.lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], L.fork_ev, 0));
         HIP_OK(hipStreamWaitEvent(L.acc_stream, L.fork_ev, 0));
@@ -1697,6 +1677,9 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         auto done_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k]; };
         auto acc_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k + 1]; };
         const bool split = ext_split(sm) || s->ext_split;
+        // the spheres mode's lean / heavy shading launches pay one more launch tail per iteration: worth it on full
+        // frames (bench 7.16 -> 7.09 ms), not on small ones (the N = 8 row share, 3.2 M samples: 1.013 -> 1.066 ms)
+        const bool split_shade = s->shade_split && (uint64_t)n_pix * N >= kSplitShadeMin;
         size_t n_ext = 0;
         for (const LaneSched& ln : f.lane) n_ext += ln.T * (split || s->split_runs ? 2 : 1);
         P.kev.assign(timed ? 2 * n_ext : 0, nullptr);
@@ -1736,15 +1719,11 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      ++ki;
                      ++path_launches;
                  };
-                 // nest-0: an iteration with only carried paths (or only camera samples) runs the
-                 // kernel compiled for that part alone (example.sdl 8.95 -> 8.41 ms); the spheres mode
-                 // keeps the merged kernel (its parts measured 2.8 % slower on the bench frame:
-                 // profiles/r4/ab/part_pick)
-#ifdef RS_EXT_W5  // dev A/B: the spheres mode picks the part kernels too (its carried part runs at 5 waves)
+                 // an iteration with only carried paths (or only camera samples) runs the kernel compiled for
+                 // that part alone: nest-0 example.sdl 8.95 -> 8.41 ms; the spheres mode's carried part runs at 5
+                 // waves (ext_min_waves), bench frame 7.58 -> 7.31 ms (profiles/r5/ab; at 4 waves its parts had
+                 // measured 2.8 % slower than the merged kernel, profiles/r4/ab/part_pick)
                  const bool pick = true;
-#else
-                 const bool pick = sm != kSmSpheres;
-#endif
 #ifdef RS_DEV_KNOBS
                  if (s->split_runs && n_new == 0 && !split && window[l]) {  // dev: the front run and the rest timed apart
                      I.run = 1;
@@ -1766,13 +1745,8 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  }
                  if (D > 0) {
                      const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + n_new + kBlock - 1) / kBlock);
-#ifdef RS_CAM_RECORDS  // dev A/B: the extend wrote the camera samples' records
-                     const bool cam = false;
-#else
-                     const bool cam = n_new > 0;
-#endif
-                     HIP_OK(launch_wfs_shade_all(ds, d_cc, d_inj + it_off[l] + t, WS, qd, s->class_mask, (uint32_t)t, D,
-                                                 ring_items, L.d_rad, b, cam, s->shade_split, sm, cs));
+                     HIP_OK(launch_wfs_shade_all(ds, WS, qd, s->class_mask, (uint32_t)t, D, ring_items, L.d_rad, b,
+                                                 split_shade, sm, cs));
                      ++path_launches;
                  }
                  // carried into t + 1: the samples injected by iterations t - depth + 2 .. t
@@ -1786,11 +1760,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  // batch k's samples have all finished: accumulate in sample order (the last batch on S,
                  // writing the frame and zeroing the counters for the next frame unless statistics read them)
                  const uint32_t planes = (uint32_t)(std::min<uint64_t>(f.B, (uint64_t)n_pix * N - (uint64_t)k * f.B) / n_pix);
-#ifdef RS_RAD_AOS  // dev A/B: item-major radiance (rs_kernels.hip put_rad)
-                 const double* rk = L.d_rad + (size_t)3 * (k % f.ring) * f.B;
-#else
-                 const double* rk = L.d_rad + (size_t)(k % f.ring) * f.B;
-#endif
+                 const double* rk = L.d_rad + (size_t)3 * (k % f.ring) * f.B;  // item-major radiance (put_rad)
                  if (k + 1 < f.n_batches) {
                      HIP_OK(hipStreamWaitEvent(L.acc_stream, done_ev(k), 0));
                      HIP_OK(launch_accumulate(rk, ring_items, L.d_acc, n_pix, planes, k == 0, 0, fp, d_out, nullptr, 0,
@@ -1823,7 +1793,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         // gen_perm). Scenes whose traversal stack spills to HBM keep one lane (the overflow array is
         // shared by blockIdx).
         uint32_t lanes = (wavefront && !ext_spill) ? std::min<uint32_t>(kMaxLanes, s->wf_lanes) : 1u;
-        uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(s->pool_paths, (uint64_t)n_pix * spb));
+        uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(pool_limit(s, R), (uint64_t)n_pix * spb));
         if (lanes > 1) {
             const uint64_t planes = (spb + lanes - 1) / lanes;
             const uint64_t split = std::max<uint64_t>(kBlock, spb >= lanes ? (uint64_t)n_pix * planes

@@ -106,14 +106,6 @@ struct InjParams {
                           // 2 the rest (dev builds time the two runs in separate launches)
 };
 
-// A frame's camera and lattice in device memory (one copy per frame), next to every iteration's InjParams:
-// the shading reads them only where it regenerates a camera sample, so the kernel keeps no registers for them
-// (as kernel arguments they raised its SGPR spills 95 -> 211 and added 68 B of VGPR scratch).
-struct CamConsts {
-    DCamera C;
-    PathParams P;
-};
-
 struct FinalParams {
     uint32_t n_pix_local, width, row_begin, row_step;
     uint32_t n_samples;
@@ -163,14 +155,12 @@ constexpr bool ext_split(int sm) { return sm == kSmNest2; }
 hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                              uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
                              int part, int sm, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present; cc / inj
-// (device memory): the frame's camera and the iteration's injection (its camera samples are regenerated, not
-// read back); ring: the rad channel stride
-// cam: the iteration injects camera samples (the launch regenerates them); split: the spheres mode's lean and heavy
-// material classes in two launches (k_wfs_shade_all PS)
-hipError_t launch_wfs_shade_all(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
-                                uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
-                                uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, int sm, hipStream_t st);
+// every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present; ring: the
+// rad ring's items (batch buffers x batch items)
+// split: the spheres mode's lean and heavy material classes in two launches (k_wfs_shade_all PS)
+hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
+                                uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, int sm,
+                                hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
 hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
 hipError_t launch_combine(float* acc, const float* nw, uint64_t n, float p, hipStream_t st);

@@ -77,16 +77,11 @@ __device__ __forceinline__ T nld(const void* base, uint32_t byte_off) {
     else return gld<T>(base, byte_off);
 }
 
-// A sample's radiance in a rad buffer: channel-major (channel c of item at c * stride + item) or, with
-// RS_RAD_AOS (dev A/B), item-major (3 doubles per item: a scattered end-of-path write touches one line)
-__device__ __forceinline__ void put_rad(double* __restrict__ rad, uint64_t stride, uint64_t item, double r, double g,
-                                        double b) {
-#ifdef RS_RAD_AOS
-    (void)stride;
+// A sample's radiance in a rad buffer, item-major (3 doubles per item): a path that ends deep in the frame
+// writes its radiance to a scattered item, and the three channels then share one line (channel-major
+// buffers took three: bench frame 7.58 -> 7.43 ms, profiles/r5/ab). k_accumulate reads them pixel-major.
+__device__ __forceinline__ void put_rad(double* __restrict__ rad, uint64_t item, double r, double g, double b) {
     rad[3 * item] = r; rad[3 * item + 1] = g; rad[3 * item + 2] = b;
-#else
-    rad[item] = r; rad[stride + item] = g; rad[2 * stride + item] = b;
-#endif
 }
 
 #ifdef RS_TRAV_STATS  // dev builds only (tools/build_variant.sh -DRS_TRAV_STATS): traversal counters
@@ -603,7 +598,7 @@ __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, flo
 // World::hit of a flat scene with a 4-wide tree through queued leaf passes (above). q: this lane's
 // column of the block's FIFO array (RS_LEAFQ x kBlock ints). Every lane of the wave that calls it
 // must call it (the pass choice is a ballot over the calling lanes).
-template <int SM, class STK, bool TOUT = false>
+template <int SM, class STK>
 __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk,
                                                int* q) {
     const RayC rc = ray_consts(r);
@@ -647,7 +642,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
     s_st_leaves[threadIdx.x] = st_leaves;
     s_st_witer[threadIdx.x] = st_witer;
 #endif
-    bend_out = TOUT ? best : bend;
+    bend_out = bend;
     return (bp >= 0 && S.lprim) ? S.lprim[bp] : bp;
 }
 
@@ -739,13 +734,10 @@ __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, 
 template <int SM, class STK, bool LOBJ = false, bool TOUT = false>
 __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if (S.root < 0) return -1;
-    // nest-0 only: on nest-2 (C4's scene) the split walk measured 2 % slower, on nest-0 (example.sdl)
-    // 2.5 % faster (profiles/r4/ab/deferred_leaves)
-#ifdef RS_NEST2_DEFER  // dev A/B: nest-2 scenes with an LDS image walk with deferred leaf tests too
+    // the nest modes with an LDS image: example.sdl 2.5 % faster (profiles/r4/ab/deferred_leaves); C4's scene
+    // 2 % slower in round 4, 14 % faster since the nested-object registers were cut (the walk's and the tests'
+    // registers are never live together: scratch 184 -> 144 B at 3 waves; profiles/r5/ab/c4_variants_r5c.jsonl)
     if constexpr (LOBJ && (SM == kSmNest0 || SM == kSmNest2)) return traverse_deferred<SM>(S, r, tmin, bend_out, stk);
-#else
-    if constexpr (LOBJ && SM == kSmNest0) return traverse_deferred<SM>(S, r, tmin, bend_out, stk);
-#endif
     const RayC rc = ray_consts(r);
     const RayF rf = make_rayf(r.o, rc.inv);
     const float tmin32 = -round_up_f(-tmin);
@@ -1093,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void k_path_mega(const DScene* __restrict__
             Ray r = camera_ray(C, u, v, rng);
             L = trace_path<SM>(S, r, P.depth, rng, stk, segs);
         }
-        put_rad(rad, P.n_items, item, L.x, L.y, L.z);
+        put_rad(rad, item, L.x, L.y, L.z);
     }
     // wave-reduce the segment count, one atomic per wave, spread over 256 counters
     unsigned long long s64 = segs;
@@ -1248,14 +1240,6 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
     camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
     return true;
 }
-// camera_sample of an item known to be live (the shading's regeneration of a traced camera sample)
-__device__ __forceinline__ void camera_sample_xy_item(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
-    const uint32_t pl = (uint32_t)(item % P.n_pix_local);
-    const uint32_t sl = (uint32_t)(item / P.n_pix_local);
-    const uint32_t x = pl % P.width;
-    const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
-    camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
-}
 
 // Camera-ray order: the i-th camera sample a launch traces is item gen_perm(i) of its batch (whole
 // sample planes). Within each plane the lattice pixels are visited in TW x TH tiles (TW * TH = 64:
@@ -1294,8 +1278,7 @@ __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_
 }
 
 // The camera sample behind the streaming iteration's injected record jg (0-based among its injections):
-// its frame item g (camera_sample) and its radiance slot in the rad ring. The extend generates the sample
-// from it and the shading regenerates it the same way (no path record is written for a camera sample).
+// its frame item g (camera_sample) and its radiance slot in the rad ring.
 __device__ __forceinline__ void inj_sample(const InjParams& I, const PathParams& P, uint32_t jg, uint64_t& g,
                                            uint32_t& item) {
     uint32_t jb = I.jb0 + jg, nb = I.nb0;
@@ -1318,7 +1301,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
     if (i < n) {
         item = item0 + gen_perm(i, item0, n, P);
         live = camera_sample(C, P, item, r, rng);
-        if (!live) put_rad(rad, P.n_items, item, 0.0, 0.0, 0.0);
+        if (!live) put_rad(rad, item, 0.0, 0.0, 0.0);
     }
     if (!P.mask && P.depth > 0) {
         // no pixel mask: every camera sample is live, so record i is thread i's (no compaction, and
@@ -1389,7 +1372,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ 
                 L = close_path(L, T);
                 alive = false;
             }
-            if (!alive) put_rad(rad, n_items, item, L.x, L.y, L.z);
+            if (!alive) put_rad(rad, item, L.x, L.y, L.z);
         }
         const uint32_t slot = block_slot1(alive, &W.counts[bounce + 1]);
         if (alive) store_path(nxt, slot, r, T, rng, item);
@@ -1421,11 +1404,11 @@ constexpr int kClsLight = 6;
 // 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 with the LDS image 3 (168 VGPRs, 184 B
 // of scratch: 4 % faster than 2 waves, 4 waves 12 % slower; profiles/r4/ab/nest2_registers), nest-2
 // with its tables in global memory 2 (its loads are L1 / L2 round trips that the spills would join)
+// The spheres mode's carried-path part (the divergent bounce >= 1 rays: lane efficiency 0.51 for BSDF rays,
+// profiles/r5/iters) at 5 waves: 96 VGPRs, 12 B of scratch, 5 blocks of 24 KiB stacks per CU; bench frame
+// 7.58 -> 7.31 ms. Its camera part keeps 4 (13 VGPRs would spill).
 constexpr int ext_min_waves(int sm, bool lobj = false, int part = kExtAll) {
-#ifdef RS_EXT_W5  // dev A/B: the spheres mode's carried-path extend at 5 waves (96 VGPRs, 12 B of scratch)
     if (sm == kSmSpheres && part == kExtCarried) return 5;
-#endif
-    (void)part;
     return sm == kSmNest2 ? (lobj ? 3 : 2) : 4;
 }
 
@@ -1475,9 +1458,6 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
     const DScene& S = LOBJ ? Sv : *Sp;  // otherwise the scene in device memory (no by-value copy in scratch)
     __shared__ int stk_all[stack_lds(SM) * kBlock];
     const StkT<OVF, stack_lds(SM)> stk = make_stk<OVF, stack_lds(SM)>(S, stk_all);
-#ifdef RS_SPH_LEAFQ
-    __shared__ int leafq[SM == kSmSpheres ? RS_LEAFQ * kBlock : 1];
-#endif
     uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
     const uint32_t nf = cnt[cix(kCntFront)];
     const uint32_t n_old = PART == kExtCamera ? 0u : nf + cnt[cix(kCntBack)];
@@ -1504,7 +1484,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                 uint64_t g;
                 inj_sample(I, P, j - n_old, g, item);
                 live = camera_sample(C, P, g, r, rng);
-                if (!live) put_rad(rad, I.ring, item, 0.0, 0.0, 0.0);
+                if (!live) put_rad(rad, item, 0.0, 0.0, 0.0);
             } else {
                 r = load_ray(cur, i);
                 live = true;
@@ -1518,15 +1498,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
             double bend = RS_INF;
             // the spheres mode keeps the winner's t (W.hit: the shading's sphere_rec_at), the others the range end
             constexpr bool kT = SM == kSmSpheres;
-#ifdef RS_SPH_LEAFQ  // dev A/B: the spheres mode's leaves through the per-lane leaf FIFO (traverse_flat_q)
-            int bp;
-            if constexpr (SM == kSmSpheres)
-                bp = traverse_flat_q<SM, StkT<OVF, stack_lds(SM)>, true>(S, r, 0.0001, bend, stk, leafq + threadIdx.x);
-            else
-                bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ, kT>(S, r, 0.0001, bend, stk);
-#else
             const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ, kT>(S, r, 0.0001, bend, stk);
-#endif
             V3 add;
             bool done = true;
             if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
@@ -1557,12 +1529,11 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                     add = emission<0>(S, S.mats[mi >= 0 ? mi : S.default_mat], h);
                     cls = -1;
                 } else {
-                    // a carried path's record is in place; a camera sample that goes on to shading has
-                    // none (T = 1, level 0): the shading regenerates it from its slot (inj_sample)
+                    // a camera sample that goes on to shading: its record (T = 1, level 0), written from the
+                    // registers it was traced from; a carried path's is in place. (Regenerating it in the
+                    // shading instead measured 0.5 % slower on the bench frame and 5 % on C4: profiles/r5/ab.)
                     W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-#ifdef RS_CAM_RECORDS  // dev A/B: the camera sample's record written here and read back by the shading
                     if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
-#endif
                     done = false;
                 }
             }
@@ -1573,7 +1544,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                 } else {
                     t4 = cur.thr[i]; item = cur.tag[i].x;
                 }
-                put_rad(rad, I.ring, item, 0.0 + t4.x * add.x, 0.0 + t4.y * add.y, 0.0 + t4.z * add.z);
+                put_rad(rad, item, 0.0 + t4.x * add.x, 0.0 + t4.y * add.y, 0.0 + t4.z * add.z);
             }
         }
 #ifdef RS_TRAV_STATS
@@ -1597,17 +1568,10 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
 // One batch of 256 queued paths of material class KIND (-1: the generic material switch; entries
 // base .. base + 255 of a queue of n): finish the hit record, scatter, write the radiance of paths that
 // end and append the survivors to the next set. Must be called by every thread of the block (block_slot).
-// CAM (launches of iterations that inject camera samples): the injected samples (records nf .. nf + n_new - 1
-// of the set, nf = its front run) have no record -- the extend traced them from registers -- and are
-// regenerated here from their slot (inj_sample + camera_sample: the same ray and RNG state, T = 1, level 0)
-// instead of being written and read back (104 B each way per camera sample that reaches a surface). Launches
-// of iterations without injections compile none of it (the regeneration's registers spilled in them).
-template <int KIND, int SM, bool CAM>
+template <int KIND, int SM>
 __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const uint32_t* __restrict__ queue,
-                                                uint32_t n, uint32_t base, uint32_t it, uint32_t nf, uint32_t* cnt_next,
-                                                uint32_t depth, uint64_t ring, double* __restrict__ rad,
-                                                const CamConsts* __restrict__ cc, const InjParams* __restrict__ inj,
-                                                uint32_t n_new) {
+                                                uint32_t n, uint32_t base, uint32_t it, uint32_t* cnt_next, uint32_t depth,
+                                                uint64_t ring, double* __restrict__ rad) {
     const WfSet& cur = W.set[it & 1];
     const WfSet& nxt = W.set[(it + 1) & 1];
     const uint32_t j = base + threadIdx.x;
@@ -1619,18 +1583,10 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     uint32_t item = 0, lvl = 0;
     if (j < n) {
         const uint32_t i = queue[j];
-        const uint32_t jg = i - nf;
-        if (CAM && jg < n_new) {
-            uint64_t g;
-            inj_sample(*inj, cc->P, jg, g, item);
-            camera_sample_xy_item(cc->C, cc->P, g, r, rng);
-            T = v3(1.0, 1.0, 1.0);
-        } else {
-            load_path(cur, i, r, T, rng);
-            const uint2 tg = cur.tag[i];
-            item = tg.x;
-            lvl = tg.y;
-        }
+        load_path(cur, i, r, T, rng);
+        const uint2 tg = cur.tag[i];
+        item = tg.x;
+        lvl = tg.y;
         const double2 hb = W.hit[i];
         const int bp = (int)__double_as_longlong(hb.x);
         Hit h;
@@ -1650,7 +1606,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
             // None (camera.rs:172-176, 250), 0 + T * e as in shade_step
             const V3 e = emission<0>(S, M0, h);
             const V3 L = v3(0.0, 0.0, 0.0) + v3(T.x * e.x, T.y * e.y, T.z * e.z);
-            put_rad(rad, ring, item, L.x, L.y, L.z);
+            put_rad(rad, item, L.x, L.y, L.z);
             cont = false;
             item = ~0u;  // radiance written
         } else {
@@ -1664,7 +1620,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
         alive = cont && (lvl + 1 < depth);  // the depth limit of ray_color (camera.rs:161)
         if (!alive && item != ~0u) {  // absorbed or depth limit: no emission term
             const V3 L = close_path(v3(0.0, 0.0, 0.0), T);
-            put_rad(rad, ring, item, L.x, L.y, L.z);
+            put_rad(rad, item, L.x, L.y, L.z);
         }
     }
     // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
@@ -1691,23 +1647,19 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // Waves: 3; nest-2 with class 4 and the tables in global memory 1 (bounded to 3 it spilled and lost
 // 21 % on C4 in round 3; with the LDS image 3 waves measured 5 % faster than 2: nest2_registers)
 // PS: the classes of this launch -- 0 all; 1 the lean ones (Lambertian, Metal, Dielectric: bounded to 4 waves);
-// 2 the heavy ones (DiffuseMetal's two ONBs and ReflectionPdf loop, the generic switch) -- RS_SHADE_SPLIT
-template <int SM, bool G4, bool LOBJ, int PS, bool CAM>
+// 2 the heavy ones (DiffuseMetal's two ONBs and ReflectionPdf loop, the generic switch): rs_scene::shade_split
+template <int SM, bool G4, bool LOBJ, int PS>
 __global__ __launch_bounds__(kBlock, PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
-                                                                                   double* __restrict__ rad,
-                                                                                   const CamConsts* __restrict__ cc,
-                                                                                   const InjParams* __restrict__ inj) {
+                                                                                   double* __restrict__ rad) {
     // (3 waves: 171 -> 168 VGPRs; at 4 waves it spilled 156 B, +6 %; nest-2 bounded at 3 spilled: C4 -21 %)
     DScene Sv;
     if constexpr (LOBJ) lds_scene(Sp, Sv);
     const DScene& S = LOBJ ? Sv : *Sp;
     const uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
     uint32_t* cnt_next = W.counts + (size_t)(it + 1) * kWfsStride;
-    const uint32_t nf = cnt[cix(kCntFront)];  // the front run: the injected camera samples' slots follow it
-    const uint32_t n_new = inj->n_new;
     constexpr int NC = G4 ? 5 : 4;
     constexpr uint32_t kPart = PS == 0 ? 0x1fu : PS == 1 ? 0x0bu : 0x14u;  // classes of this launch
     uint32_t n[NC], first[NC + 1];
@@ -1724,19 +1676,19 @@ __global__ __launch_bounds__(kBlock, PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOB
         const uint32_t base = (v - first[k]) * kBlock;
         if (k == 0) {
             if constexpr ((kPart & 1u) != 0)
-                wfs_shade_batch<RS_MAT_LAMBERTIAN, SM, CAM>(S, W, queues[0], n[0], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+                wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], n[0], base, it, cnt_next, depth, ring, rad);
         } else if (k == 1) {
             if constexpr ((kPart & 2u) != 0)
-                wfs_shade_batch<RS_MAT_METAL, SM, CAM>(S, W, queues[1], n[1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+                wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], n[1], base, it, cnt_next, depth, ring, rad);
         } else if (k == 2) {
             if constexpr ((kPart & 4u) != 0)
-                wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM, CAM>(S, W, queues[2], n[2], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+                wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], n[2], base, it, cnt_next, depth, ring, rad);
         } else if (k == 3 || !G4) {
             if constexpr ((kPart & 8u) != 0)
-                wfs_shade_batch<RS_MAT_DIELECTRIC, SM, CAM>(S, W, queues[3], n[3], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+                wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], n[3], base, it, cnt_next, depth, ring, rad);
         } else {
             if constexpr ((kPart & 16u) != 0)
-                wfs_shade_batch<-1, SM, CAM>(S, W, queues[NC - 1], n[NC - 1], base, it, nf, cnt_next, depth, ring, rad, cc, inj, n_new);
+                wfs_shade_batch<-1, SM>(S, W, queues[NC - 1], n[NC - 1], base, it, cnt_next, depth, ring, rad);
         }
     }
 }
@@ -1755,20 +1707,12 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict_
     // (rs_host.cpp counts_clean; the host passes n_zero = 0 when it still reads them)
     for (uint64_t z = t; z < n_zero; z += (uint64_t)gridDim.x * kBlock) zero[z] = 0u;
     if (t >= 3ull * n_pix) return;
-#ifdef RS_RAD_AOS  // item-major radiance: thread 3p + c, so a wave's reads of a sample plane are contiguous
+    // thread 3p + c: a wave's reads of a sample plane of the item-major radiance are contiguous
     const uint32_t p = (uint32_t)(t / 3), c = (uint32_t)(t - 3ull * p);
-#else
-    const uint32_t c = (uint32_t)(t / n_pix), p = (uint32_t)(t - (uint64_t)c * n_pix);
-#endif
     double a = first ? 0.0 : acc[(uint64_t)c * n_pix + p];
-#ifdef RS_RAD_AOS
     const double* rc = rad + 3ull * p + c;
     const uint64_t sstep = 3ull * n_pix;
     (void)stride;
-#else
-    const double* rc = rad + (uint64_t)c * stride + p;
-    const uint64_t sstep = n_pix;
-#endif
     uint32_t s = 0;
     for (; s + 16 <= n_samp; s += 16) {
         double v[16];
@@ -1932,10 +1876,10 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
                                uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, \
                                int part, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1),                        \
       (s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1))                                                  \
-    X(hipError_t, wfs_shade_all, (const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w, \
-                                  uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,      \
-                                  uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, hipStream_t st), \
-      (s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks, cam, split, st))
+    X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, \
+                                  uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, \
+                                  hipStream_t st),                                                              \
+      (s, w, queues, class_mask, it, depth, ring, rad, blocks, split, st))
 #define RS_DECLARE_SM(R, NAME, PARAMS, ARGS) template <int SMC> R NAME##_sm PARAMS;
 RS_SM_LAUNCHERS(RS_DECLARE_SM)
 RS_SORTED_LAUNCHERS(RS_DECLARE_SM)
@@ -2019,26 +1963,19 @@ hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& 
 }
 
 template <int SMC>
-hipError_t wfs_shade_all_sm(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
-                            uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
-                            uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, hipStream_t st) {
+hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, uint32_t it,
+                            uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, hipStream_t st) {
     if (!blocks) return hipSuccess;
 #define RS_SHADE_LAUNCH(G4, LOBJ, PS, SHM)                                                                          \
-    do {                                                                                                        \
-        if (cam)                                                                                                \
-            hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ, PS, true>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, \
-                               queues, class_mask, it, depth, ring, rad, cc, inj);                             \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ, PS, false>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, \
-                               queues, class_mask, it, depth, ring, rad, cc, inj);                             \
-    } while (0)
+    hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ, PS>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, queues, \
+                       class_mask, it, depth, ring, rad)
     const uint32_t shm = s.host->limg_bytes;  // nest modes' LDS image (none in the spheres mode)
     if constexpr (SMC == kSmNest0 || SMC == kSmNest2) {
         if (class_mask & (1u << 4)) { if (shm) RS_SHADE_LAUNCH(true, true, 0, shm); else RS_SHADE_LAUNCH(true, false, 0, 0); }
         else { if (shm) RS_SHADE_LAUNCH(false, true, 0, shm); else RS_SHADE_LAUNCH(false, false, 0, 0); }
     } else if (split) {
         // the lean classes (Lambertian, Metal, Dielectric) at 4 waves, then the heavy ones (DiffuseMetal, the
-        // generic switch) at 3: the merged kernel's registers are DiffuseMetal's (168), Lambertian alone 133
+        // generic switch) at 3: the merged kernel's registers are DiffuseMetal's (168), Lambertian's alone 133
         RS_SHADE_LAUNCH(false, false, 1, 0);
         if (class_mask & 0x14u) {
             if (class_mask & (1u << 4)) RS_SHADE_LAUNCH(true, false, 2, 0);
@@ -2107,11 +2044,10 @@ hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathPara
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_wfs_shade_all(const SceneRef& s, const CamConsts* cc, const InjParams* inj, const WfState& w,
-                                uint32_t* const* queues, uint32_t class_mask, uint32_t it, uint32_t depth,
-                                uint64_t ring, double* rad, uint32_t blocks, bool cam, bool split, int sm, hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, cc, inj, w, queues, class_mask, it, depth, ring, rad, blocks,
-                                                           cam, split, st));
+hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
+                                uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, int sm,
+                                hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, it, depth, ring, rad, blocks, split, st));
     return hipErrorInvalidValue;
 }
 

@@ -37,15 +37,16 @@ def main():
             f = []
     per_it = defaultdict(lambda: defaultdict(list))
     for fr in fl[1:]:
-        t, es = 0, []
+        # an iteration: its extend launches, then its shading launches (one, or the split shading's two)
+        its, prev = [], None
         for kind, d in fr:
-            if kind == "E":
-                es.append(d)
-            else:
-                per_it[t]["E"].append(es)
-                per_it[t]["S"].append(d)
-                t += 1
-                es = []
+            if kind == "E" and prev != "E":
+                its.append(([], []))
+            its[-1][0 if kind == "E" else 1].append(d)
+            prev = kind
+        for t, (es, ss) in enumerate(its):
+            per_it[t]["E"].append(es)
+            per_it[t]["S"].append(sum(ss))
     counts = frames[-1] if frames else []
     print(f"{'t':>2} {'front':>9} {'back':>9} {'camera':>9} {'shaded':>9} {'ended':>9} | {'ext front us':>12} {'ps/ray':>7} "
           f"{'ext rest us':>12} {'ps/ray':>7} {'shade us':>9} {'ps/path':>7}")
