@@ -275,6 +275,8 @@ struct rs_scene {
     // by its device memory (Replica::pool_limit)
     uint64_t pool_paths = 256ull << 20;
     uint32_t inject_div = 1;                      // streaming: inject up to 1/inject_div of a lane per iteration
+    uint32_t finish_after = 16;                   // streaming: wavefront iterations after the last injection before
+                                                  // the finish launch (k_wfs_finish; 0: none; never on nest-2 scenes)
     uint32_t wf_lanes = 2;                        // chunk lanes of the bounce-synchronous wavefront (rs_scene_set_lanes)
     uint32_t stream_lanes = 1;                    // lanes of the streaming wavefront (rs_scene_set_lanes)
     uint32_t frames_in_flight = 2;                // frame slots per replica (rs_scene_set_frames_in_flight)
@@ -1071,6 +1073,7 @@ void build(rs_scene* s) {
     stage(s, d.pbox, pboxes);
     stage(s, d.pclass, pclass);
     d.root4 = -1;
+    d.ltop = 0;
     s->tree_arity = root >= 0 ? 2 : 0;
     s->n_nodes = B.nodes.size();
     // the binary tree is walked in reference order by ref_order scenes and, whatever ref_order says,
@@ -1085,14 +1088,37 @@ void build(rs_scene* s) {
         if (r4 >= 0) {
             // the kernels address nodes with 32-bit byte offsets (rs_kernels.hip gld)
             if (n4.size() * sizeof(DNode4) > 0xFFFFFFFFull) throw Error(RS_E_INVALID, "scene too large: 4-wide tree over 4 GiB");
+            s->stack_need = stack_need4(n4, r4);
+            int32_t root_id = r4;
+            d.ltop = 0;
+            if (s->scene_mode == kSmSpheres) {
+                // breadth-first node order: the tree's top levels are nodes 0 .. kLTop - 1, which the extend's blocks
+                // also hold in LDS (d.ltop); the order changes no hit (near-first traversal of the same tree)
+                std::vector<int32_t> order, newid(n4.size(), -1);
+                order.push_back(r4);
+                newid[r4] = 0;
+                for (size_t q = 0; q < order.size(); ++q)
+                    for (int k = 0; k < 4; ++k) {
+                        const int32_t c = n4[order[q]].child[k];
+                        if (c >= 0) { newid[c] = (int32_t)order.size(); order.push_back(c); }
+                    }
+                std::vector<HNode4> bfs(order.size());
+                for (size_t q = 0; q < order.size(); ++q) {
+                    bfs[q] = n4[order[q]];
+                    for (int k = 0; k < 4; ++k)
+                        if (bfs[q].child[k] >= 0) bfs[q].child[k] = newid[bfs[q].child[k]];
+                }
+                n4.swap(bfs);
+                root_id = 0;
+                d.ltop = (int32_t)std::min<size_t>(n4.size(), (size_t)kLTop);
+            }
             std::vector<DNode4> dn4;
             for (const HNode4& h : n4) dn4.push_back(to_device4(h));
             stage(s, d.nodes4, dn4);
-            d.root4 = r4;
+            d.root4 = root_id;
             s->tree_arity = 4;
             s->tree_depth = depth4;
             s->n_nodes = n4.size();
-            s->stack_need = stack_need4(n4, r4);
         }
     }
     // reference-order scenes on the in-order 4-wide tree (collapse4_inorder), nest-0 / nest-2 modes (the
@@ -1389,6 +1415,7 @@ struct LaneSched {
     uint64_t cnt_off = 0;               // the lane's counter blocks in the frame's counter array (words)
     uint64_t B = 0, last_nb = 0;        // batch size, size of the lane's last batch
     uint32_t D = 0;
+    bool finish = false;                // the last iteration traces every carried path to its end (k_wfs_finish)
     uint64_t nb(uint64_t m) const { return m + 1 == batch.size() ? last_nb : B; }
     uint64_t first_it(uint64_t m) const { return (m * B) / Q; }
     uint64_t done_it(uint64_t m) const {
@@ -1454,6 +1481,18 @@ FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D,
         L.Q = q;
         L.T_inj = (L.total + q - 1) / q;
         L.T = L.T_inj + (D ? D - 1 : 0);
+        // the finish: after the last injection, finish_after wavefront iterations, then one launch that traces
+        // every path still carried to its end (a depth-50 frame's last ~40 iterations carry a few thousand paths
+        // each and cost their launch gaps and one traversal's latency apiece). Measured (finish_after 0 / 4 / 8 /
+        // 12, profiles/r5/ab/finish_after_r5e.jsonl): example.sdl 800x500x64 8.51 / 10.63 / 8.46 / 8.01 ms, RTIOW
+        // 1920x1080x64 47.96 / 58.54 / 46.52 / 44.54 ms; 12 / 16 / 24 (finish_after_r5f.jsonl): 8.03 / 7.62 / 7.77
+        // and 44.30 / 44.06 / 44.73 ms -- but quadric.sdl (9 segments per sample: many paths
+        // still alive, and the finish runs them one thread each at 2 waves) 113.6 / 182.5 / 157.8 / 144.7 ms, so
+        // nest-2 scenes do not finish
+        if (s->finish_after && s->scene_mode != kSmNest2 && L.T > L.T_inj + s->finish_after + 1) {
+            L.finish = true;
+            L.T = L.T_inj + s->finish_after + 1;
+        }
         L.cap = bound(q);
         L.cnt_off = f.n_counts;
         f.n_counts += (L.T + 1) * kWfsStride;
@@ -1711,6 +1750,15 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                          if (ln.first_it(mm) == t && kk >= f.ring) HIP_OK(hipStreamWaitEvent(cs, acc_ev(kk - f.ring), 0));
                      }
                  }
+                 if (ln.finish && t + 1 == ln.T) {  // the finish: every carried path to its end, one launch
+                     const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + kBlock - 1) / kBlock);
+                     HIP_OK(launch_wfs_finish(ds, WS, (uint32_t)t, D, L.d_rad, std::max<uint32_t>(1, b), sm, cs));
+                     ++path_launches;
+                     window[l] = 0;
+                     while (m_done[l] < ln.batch.size() && ln.done_it(m_done[l]) == t)
+                         HIP_OK(hipEventRecord(done_ev(ln.batch[m_done[l]++]), cs));
+                     return;
+                 }
                  auto extend = [&](int part, uint64_t n_max) {
                      const uint32_t b = (uint32_t)std::min<uint64_t>(ext_cap, (n_max + kBlock - 1) / kBlock);
                      if (!b) return;
@@ -1951,6 +1999,13 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
                 for (uint32_t k = 0; k < kStatLines; ++k) live_new += q[cix(kCntStat0 + (int)k)];
                 for (int k = 0; k < kWfsClasses; ++k) shaded += q[cix(1 + k)];
                 const uint64_t old = q[cix(0)], live = old + live_new;
+                if (P.lanes[l].finish && t + 1 == P.lanes[l].T) {
+                    // the finish: its carried paths' first segments and (stat lines) the ones after; a record in
+                    // (104 B) and a radiance out (24 B) per path
+                    seg += live;
+                    kbytes += 128ull * old;
+                    continue;
+                }
                 const uint64_t dead_new = P.inj[l][t] - live_new;
                 const uint64_t ended = live - shaded;
                 seg += live;
@@ -2259,6 +2314,7 @@ int rs_scene_create(rs_scene** out) {
         v = s->max_items_per_batch; knob("RS_MAX_BATCH_ITEMS", v); s->max_items_per_batch = v;
         v = s->pool_paths; knob("RS_POOL_PATHS", v); s->pool_paths = v;
         v = s->inject_div; knob("RS_INJECT_DIV", v); s->inject_div = (uint32_t)v;
+        if (const char* e = std::getenv("RS_FINISH_AFTER")) s->finish_after = (uint32_t)std::strtoul(e, nullptr, 10);
         v = s->wf_lanes; knob("RS_LANES", v); s->wf_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
         v = s->stream_lanes; knob("RS_SLANES", v); s->stream_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
         v = s->frames_in_flight; knob("RS_FRAMES", v); s->frames_in_flight = (uint32_t)std::min<unsigned long long>(v, kMaxSlots);

@@ -33,12 +33,12 @@ constexpr int rich_of(int sm) { return sm == kSmGeneric ? 1 : 0; }
 // the streaming (material-sorted) wavefront serves these modes; flat (mesh) and generic scenes run
 // the bounce-synchronous unsorted wavefront
 constexpr bool streaming_mode(int sm) { return sm == kSmSpheres || sm == kSmNest0 || sm == kSmNest2; }
-// LDS stack entries per thread of the path kernels (k_wf_extend, k_wfs_extend) by scene mode: 16 for
-// meshes and nested objects, 24 elsewhere. A 32 KiB block (24 entries + the mesh extend's 8-entry leaf
-// FIFO) kept only 4 of the flat extend's 5 blocks per CU resident; at 16 entries the C5 mesh frame is
-// 10 % faster although more of its deep entries spill to HBM, C4 2.5 % and example.sdl 1.6 %; the
-// rich mode (X2) lost 4 % and the spheres mode is unchanged (profiles/r4/ab/lds_stack).
-constexpr int stack_lds(int sm) { return (sm == kSmFlat || sm == kSmNest0 || sm == kSmNest2) ? kStackMin : kStackMax; }
+// LDS stack entries per thread of the path kernels (k_wf_extend, k_wfs_extend) by scene mode: 16, 24 in the
+// rich mode. A 32 KiB block (24 entries + the mesh extend's 8-entry leaf FIFO) kept only 4 of the flat extend's
+// 5 blocks per CU resident; at 16 entries the C5 mesh frame is 10 % faster although more of its deep entries
+// spill to HBM, C4 2.5 % and example.sdl 1.6 %; the rich mode (X2) lost 4 % (profiles/r4/ab/lds_stack). The
+// spheres mode takes 16 since round 5: its extend's LDS tree top (kLTop) then fits 5 blocks per CU.
+constexpr int stack_lds(int sm) { return sm == kSmGeneric ? kStackMax : kStackMin; }
 // the nest modes' LDS scene image (rs_layout.h kLimgMax) next to their stack: four 256-thread blocks per CU
 // must fit the CU's 160 KiB of LDS
 static_assert(4u * ((uint32_t)stack_lds(kSmNest0) * kBlock * 4u + kLimgMax) <= 160u * 1024u, "LDS image budget");
@@ -157,6 +157,10 @@ hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathPara
                              int part, int sm, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present; ring: the
 // rad ring's items (batch buffers x batch items)
+// the streaming frame's last iteration: every carried path of set it&1 traced to its end, one thread each
+// (k_wfs_finish); blocks: at least one per 256 carried paths (grid-stride)
+hipError_t launch_wfs_finish(const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad, uint32_t blocks,
+                             int sm, hipStream_t st);
 // split: the spheres mode's lean and heavy material classes in two launches (k_wfs_shade_all PS)
 hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
                                 uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, int sm,

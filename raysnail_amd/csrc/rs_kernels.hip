@@ -438,7 +438,11 @@ __device__ __forceinline__ void trav_stats_flush(bool live, int st_cat = 0) {
 #define RS_ST_PARAMS
 #define RS_ST_PASS
 #endif
-template <int SM, class STK, bool LOBJ = false>
+// The spheres mode's tree top in LDS (TOP): the extend's blocks copy nodes 0 .. S.ltop - 1 of the breadth-first
+// tree here; a node step whose wave is entirely inside the top reads its node with ds_read (a wave-uniform choice,
+// so no lane waits on both paths), the others from the global copy.
+__shared__ DNode4 s_top4[kLTop > 0 ? kLTop : 1];
+template <int SM, class STK, bool LOBJ = false, bool TOP = false>
 __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const RayC& rc, const RayF4& rq, double tmin,
                                  float tmin32, int node, int& sp, const STK& stk, double& best, double& bend,
                                  int& bp, float& best32 RS_ST_PARAMS) {
@@ -456,7 +460,13 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
     } while (0)
     f4v NX, FX, NY, FY, NZ, FZ;
     i4v NC;
-    load_node4<LOBJ>(S, rq, node, NX, FX, NY, FY, NZ, FZ, NC);
+    if (TOP && __ballot(node >= S.ltop) == 0ull) {
+        DScene T = S;
+        T.nodes4 = s_top4;
+        load_node4<true>(T, rq, node, NX, FX, NY, FY, NZ, FZ, NC);
+    } else {
+        load_node4<LOBJ>(S, rq, node, NX, FX, NY, FY, NZ, FZ, NC);
+    }
     // per slot: inner-child code and entry (or -inf = not to visit); leaf codes are collected
     // and tested after the four box tests, when the node's registers are dead. Branch-free:
     // all four boxes are tested (the node's loads issue together) and the slot results are
@@ -731,7 +741,7 @@ __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, 
 // call measured slower in round 3, profiles/r3/ab/generic_inline_*.txt)
 // TOUT: bend_out receives the winner's own t (best) instead of the range end it was accepted under (the spheres
 // mode's shading rebuilds the record from t: sphere_rec_at)
-template <int SM, class STK, bool LOBJ = false, bool TOUT = false>
+template <int SM, class STK, bool LOBJ = false, bool TOUT = false, bool TOP = false>
 __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     if (S.root < 0) return -1;
     // the nest modes with an LDS image: example.sdl 2.5 % faster (profiles/r4/ab/deferred_leaves); C4's scene
@@ -808,7 +818,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const Ray& r, double tm
         node = S.root4;
         while (node >= 0) {
             RS_ST_NODE();
-            node = bvh4_step<SM, STK, LOBJ>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
+            node = bvh4_step<SM, STK, LOBJ, TOP>(S, r, rc, rq, tmin, tmin32, node, sp, stk, best, bend, bp, best32 RS_ST_PASS);
         }
     } else {
         // (the generic mode's reference-order scenes: boxes / quadrics / CSG in rich scenes) BVH::hit's
@@ -1458,6 +1468,8 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
     const DScene& S = LOBJ ? Sv : *Sp;  // otherwise the scene in device memory (no by-value copy in scratch)
     __shared__ int stk_all[stack_lds(SM) * kBlock];
     const StkT<OVF, stack_lds(SM)> stk = make_stk<OVF, stack_lds(SM)>(S, stk_all);
+    // the spheres mode reads its tree top from LDS (s_top4)
+    constexpr bool kTop = SM == kSmSpheres && kLTop > 0;
     uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
     const uint32_t nf = cnt[cix(kCntFront)];
     const uint32_t n_old = PART == kExtCamera ? 0u : nf + cnt[cix(kCntBack)];
@@ -1491,14 +1503,21 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
             }
         }
         // the LDS image is filled once the block's first records are requested: their latency and the
-        // image's overlap at the barrier
+        // image's overlap at the barrier (the spheres mode's tree top likewise)
         if constexpr (LOBJ)
             if (base == base0) lds_fill(S);
+        if constexpr (kTop)
+            if (base == base0) {
+                const uint32_t nq = (uint32_t)S.ltop * (sizeof(DNode4) / 16);
+                const uint4* __restrict__ src = (const uint4*)S.nodes4;
+                for (uint32_t q = threadIdx.x; q < nq; q += kBlock) ((uint4*)s_top4)[q] = src[q];
+                __syncthreads();
+            }
         if (live) {
             double bend = RS_INF;
             // the spheres mode keeps the winner's t (W.hit: the shading's sphere_rec_at), the others the range end
             constexpr bool kT = SM == kSmSpheres;
-            const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ, kT>(S, r, 0.0001, bend, stk);
+            const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ, kT, kTop>(S, r, 0.0001, bend, stk);
             V3 add;
             bool done = true;
             if (bp < 0) {  // sky miss: L + T * background (camera.rs:253-254)
@@ -1563,6 +1582,57 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                                                    PART == kExtCarried ? nullptr : &cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))]);
         if (cls >= 0) queues[cls][slot] = i;
     }
+}
+
+// The streaming frame's finish (its last iteration, rs_host.cpp FrameSched: after the last injection and
+// kFinishAfter wavefront iterations): every path still carried (set it&1, front and back runs) is traced to its
+// end by one thread -- ray_color's remaining levels as the megakernel's trace_path runs them (world_hit +
+// shade_step; a live path's radiance so far is 0, so the result is the same 0 + T * term as the wavefront's) --
+// in one launch instead of depth - kFinishAfter small iterations whose launch gaps and per-launch latency the
+// few surviving paths of a depth-50 frame would pay. Segments beyond each path's first go to the iteration's
+// statistics lines (its first is counted as carried, cnt[0]).
+// (bounded to 2 waves: unbounded, the nest-2 instance took 256 VGPRs + 10 AGPRs at one wave per SIMD)
+template <int SM, bool LOBJ>
+__global__ __launch_bounds__(kBlock, 2) void k_wfs_finish(const DScene* __restrict__ Sp, WfState W, uint32_t it, uint32_t depth,
+                                                      double* __restrict__ rad) {
+    DScene Sv;
+    if constexpr (LOBJ) lds_scene(Sp, Sv);
+    const DScene& S = LOBJ ? Sv : *Sp;
+    __shared__ int stk_all[stack_lds(SM) * kBlock];
+    const StkT<true, stack_lds(SM)> stk = make_stk<true, stack_lds(SM)>(S, stk_all);
+    uint32_t* cnt = W.counts + (size_t)it * kWfsStride;
+    const uint32_t nf = cnt[cix(kCntFront)];
+    const uint32_t n = nf + cnt[cix(kCntBack)];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n;  // paths carried in (stats)
+    const WfSet& cur = W.set[it & 1];
+    uint32_t extra = 0;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t j = base + threadIdx.x;
+        if (j >= n) continue;
+        const uint32_t i = j < nf ? j : W.cap - 1u - (j - nf);
+        Ray r;
+        V3 T;
+        Rng rng;
+        load_path(cur, i, r, T, rng);
+        const uint2 tg = cur.tag[i];
+        V3 L = v3(0.0, 0.0, 0.0);
+        bool open = true;
+        for (uint32_t lvl = tg.y; lvl < depth; ++lvl) {
+            if (lvl != tg.y) ++extra;
+            Hit h;
+            double bend;
+            const int bp = traverse<SM, StkT<true, stack_lds(SM)>, LOBJ>(S, r, 0.0001, bend, stk);  // world_hit
+            const bool ok = finish_hit<SM>(S, bp, r, 0.0001, bend, h);
+            if (!shade_step<SM>(S, ok, h, r, T, L, rng)) { open = false; break; }
+        }
+        if (open) L = close_path(L, T);  // depth limit: the next level would return 0
+        put_rad(rad, tg.x, L.x, L.y, L.z);
+    }
+    // the extra segments, one atomic per wave on the iteration's statistics lines
+    unsigned long long e = extra;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) e += __shfl_xor(e, off, 64);
+    if ((threadIdx.x & 63) == 0 && e) atomicAdd(&cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))], (uint32_t)e);
 }
 
 // One batch of 256 queued paths of material class KIND (-1: the generic material switch; entries
@@ -1876,6 +1946,8 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
                                uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, \
                                int part, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1),                        \
       (s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1))                                                  \
+    X(hipError_t, wfs_finish, (const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad,        \
+                               uint32_t blocks, hipStream_t st), (s, w, it, depth, rad, blocks, st))              \
     X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, \
                                   uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, \
                                   hipStream_t st),                                                              \
@@ -1963,6 +2035,21 @@ hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& 
 }
 
 template <int SMC>
+hipError_t wfs_finish_sm(const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad, uint32_t blocks,
+                         hipStream_t st) {
+    if (!blocks) return hipSuccess;
+    const uint32_t shm = s.host->limg_bytes;  // nest modes' LDS image
+    if constexpr (SMC == kSmNest0 || SMC == kSmNest2) {
+        if (shm) {
+            hipLaunchKernelGGL((k_wfs_finish<SMC, true>), dim3(blocks), dim3(kBlock), shm, st, s.dev, w, it, depth, rad);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_wfs_finish<SMC, false>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, it, depth, rad);
+    return hipGetLastError();
+}
+
+template <int SMC>
 hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, uint32_t it,
                             uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, hipStream_t st) {
     if (!blocks) return hipSuccess;
@@ -2041,6 +2128,12 @@ hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathPara
                              uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
                              int part, int sm, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     RS_SM_SORTED_DISPATCH(sm, return wfs_extend_sm<SMC>(s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1));
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_wfs_finish(const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad, uint32_t blocks,
+                             int sm, hipStream_t st) {
+    RS_SM_SORTED_DISPATCH(sm, return wfs_finish_sm<SMC>(s, w, it, depth, rad, blocks, st));
     return hipErrorInvalidValue;
 }
 

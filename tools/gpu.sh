@@ -75,6 +75,7 @@ for s in "$@"; do
       (cd $R/base && step 240 python3 bench.py $B > $OUT/v_base_$rep.json 2> $OUT/v.err) || { echo "base bench failed"; tail -5 $OUT/v.err; exit 1; }
       (cd $R && step 240 python3 bench.py $B > $OUT/v_prod_$rep.json 2> $OUT/v.err) || { echo "bench failed"; tail -5 $OUT/v.err; exit 1; }
       for v in $R/raysnail_amd/lib/var_*.so; do
+        [ -e "$v" ] || continue
         n=$(basename $v .so)
         (cd $R && RS_HIP_LIB=$v step 240 python3 bench.py $B > $OUT/v_${n}_$rep.json 2> $OUT/v.err) || { echo "$n bench failed"; tail -5 $OUT/v.err; exit 1; }
       done
@@ -102,8 +103,18 @@ for s in "$@"; do
   c4)
     # C4-shaped frames (quadric.sdl + Cornell emitter 1024x1024, 64 spp, depth 50) with the product and every variant
     for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      [ -e "$v" ] || continue
       (cd $R && step 300 python3 tools/time_scene.py $v quadric 64 50 1024x1024 >> $OUT/c4.jsonl 2>> $OUT/c4.err) || { echo "c4 $v failed"; tail -5 $OUT/c4.err; exit 1; }
       echo "c4: $(tail -1 $OUT/c4.jsonl)"
+    done ;;
+  finish)
+    # depth-50 frames with the dev library at several finish points (RS_FINISH_AFTER: wavefront iterations after the
+    # last injection before k_wfs_finish; 0 = none): C2, a C3-shaped RTIOW frame, C4-shaped quadric frames
+    for fa in ${FINISH_AFTER:-0 4 8 12}; do
+      for sc in "example 64 50 800x500" "rtow 64 50 1920x1080" "quadric 64 50 1024x1024"; do
+        (cd $R && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_FINISH_AFTER=$fa step 300 python3 tools/time_scene.py $R/raysnail_amd/lib/libraysnail_hip_dev.so $sc >> $OUT/finish.jsonl 2>> $OUT/finish.err) || { echo "finish $fa $sc failed"; tail -5 $OUT/finish.err; exit 1; }
+        echo "finish_after $fa: $(tail -1 $OUT/finish.jsonl)"
+      done
     done ;;
   abtrace)
     # kernel traces of the bench frames (tools/render_once.py, 5 frames): the baseline worktree base/, then this tree
