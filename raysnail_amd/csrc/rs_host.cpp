@@ -1716,8 +1716,9 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         auto done_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k]; };
         auto acc_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k + 1]; };
         const bool split = ext_split(sm) || s->ext_split;
-        // the spheres mode's lean / heavy shading launches pay one more launch tail per iteration: worth it on full
-        // frames (bench 7.16 -> 7.09 ms), not on small ones (the N = 8 row share, 3.2 M samples: 1.013 -> 1.066 ms)
+        // lean / heavy shading launches (spheres mode; nest modes with an LDS image) pay one more launch tail per
+        // iteration: worth it on full frames (bench 7.16 -> 7.09 ms), not on small ones (the N = 8 row share, 3.2 M
+        // samples: 1.013 -> 1.066 ms)
         const bool split_shade = s->shade_split && (uint64_t)n_pix * N >= kSplitShadeMin;
         size_t n_ext = 0;
         for (const LaneSched& ln : f.lane) n_ext += ln.T * (split || s->split_runs ? 2 : 1);

@@ -2058,6 +2058,17 @@ hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const
                        class_mask, it, depth, ring, rad)
     const uint32_t shm = s.host->limg_bytes;  // nest modes' LDS image (none in the spheres mode)
     if constexpr (SMC == kSmNest0 || SMC == kSmNest2) {
+        // with the LDS image: the lean classes (leaf objects, classes 0-3 but DiffuseMetal) at 4 waves (128 VGPRs, 44 B
+        // of scratch), then DiffuseMetal and the composites (class 4: the nested-object record) at 3 (C4-shaped frame
+        // 113.2 -> 111.8 ms, profiles/r5/ab/c4_split_r5h.jsonl)
+        if (split && shm) {
+            RS_SHADE_LAUNCH(false, true, 1, shm);
+            if (class_mask & 0x14u) {
+                if (class_mask & (1u << 4)) RS_SHADE_LAUNCH(true, true, 2, shm);
+                else RS_SHADE_LAUNCH(false, true, 2, shm);
+            }
+            return hipGetLastError();
+        }
         if (class_mask & (1u << 4)) { if (shm) RS_SHADE_LAUNCH(true, true, 0, shm); else RS_SHADE_LAUNCH(true, false, 0, 0); }
         else { if (shm) RS_SHADE_LAUNCH(false, true, 0, shm); else RS_SHADE_LAUNCH(false, false, 0, 0); }
     } else if (split) {
