@@ -1091,17 +1091,22 @@ void build(rs_scene* s) {
             s->stack_need = stack_need4(n4, r4);
             int32_t root_id = r4;
             d.ltop = 0;
+            // (the flat mode's extend with a 21-node top in LDS measured 1.8 % slower on C5: profiles/r5/configs_r5k.jsonl)
             if (s->scene_mode == kSmSpheres) {
-                // breadth-first node order: the tree's top levels are nodes 0 .. kLTop - 1, which the extend's blocks
-                // also hold in LDS (d.ltop); the order changes no hit (near-first traversal of the same tree)
+                // the tree's top levels first, breadth-first (nodes 0 .. ltop - 1, which the extend's blocks also hold
+                // in LDS: d.ltop), then the other nodes in their depth-first order (a subtree's nodes stay together);
+                // the order changes no hit (near-first traversal of the same tree)
+                const size_t K = std::min<size_t>(n4.size(), (size_t)kLTop);
                 std::vector<int32_t> order, newid(n4.size(), -1);
                 order.push_back(r4);
                 newid[r4] = 0;
-                for (size_t q = 0; q < order.size(); ++q)
-                    for (int k = 0; k < 4; ++k) {
+                for (size_t q = 0; q < order.size() && order.size() < K; ++q)
+                    for (int k = 0; k < 4 && order.size() < K; ++k) {
                         const int32_t c = n4[order[q]].child[k];
                         if (c >= 0) { newid[c] = (int32_t)order.size(); order.push_back(c); }
                     }
+                for (size_t v = 0; v < n4.size(); ++v)
+                    if (newid[v] < 0) { newid[v] = (int32_t)order.size(); order.push_back((int32_t)v); }
                 std::vector<HNode4> bfs(order.size());
                 for (size_t q = 0; q < order.size(); ++q) {
                     bfs[q] = n4[order[q]];
@@ -1110,7 +1115,7 @@ void build(rs_scene* s) {
                 }
                 n4.swap(bfs);
                 root_id = 0;
-                d.ltop = (int32_t)std::min<size_t>(n4.size(), (size_t)kLTop);
+                d.ltop = (int32_t)K;
             }
             std::vector<DNode4> dn4;
             for (const HNode4& h : n4) dn4.push_back(to_device4(h));
@@ -1990,9 +1995,10 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         kbytes = 80ull * seg;
     } else {
         // the streaming extend's library byte model, per iteration: ray records in (64 B)
-        // per carried path; hit (16 B) + queue slot (4 B) per shaded segment (camera samples are traced
-        // from registers and write no record); radiance out (24 B) per path ending in extend, + its
-        // throughput record and item in (36 B); radiance out for masked samples
+        // per carried path; hit (16 B) + queue slot (4 B) per shaded segment; the record out (96 B + item
+        // + level) per live camera sample (written after its traversal for the ones that go on to shading:
+        // an upper bound); radiance out (24 B) per path ending in extend, + its throughput record and item
+        // in (36 B); radiance out for masked samples
         for (size_t l = 0; l < P.lanes.size(); ++l)
             for (uint64_t t = 0; t < P.lanes[l].T; ++t) {
                 const uint32_t* q = &P.qc[P.lanes[l].cnt_off + t * kWfsStride];
@@ -2010,7 +2016,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
                 const uint64_t dead_new = P.inj[l][t] - live_new;
                 const uint64_t ended = live - shaded;
                 seg += live;
-                kbytes += 64ull * old + 20ull * shaded + 60ull * ended + 24ull * dead_new;
+                kbytes += 64ull * old + 20ull * shaded + 104ull * live_new + 60ull * ended + 24ull * dead_new;
 #ifdef RS_DEV_KNOBS
                 if (s->dump_iters) {
                     const uint32_t* qn = q + kWfsStride;  // the next set's runs

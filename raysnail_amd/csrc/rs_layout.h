@@ -210,8 +210,8 @@ struct DScene {
     int32_t has_media;       // 1: the scene has ConstantMedium objects (rays carry the medium key)
     int32_t stack_need;      // exact worst-case traversal stack depth of the tree in use (host-computed)
     int32_t moving;          // 1: some sphere has a nonzero speed (center_at needs the time)
-    int32_t ltop;            // spheres mode: the first ltop nodes of nodes4 (breadth-first order, root 0) are the
-                             // tree's top, which the extend's blocks also hold in LDS (rs_kernels.hip s_top4); 0: none
+    int32_t ltop;            // spheres mode: the first ltop nodes of nodes4 (breadth-first, root 0) are the tree's
+                             // top, which the extend's blocks also hold in LDS (rs_kernels.hip s_top4); 0: none
     float bg_lo[4], bg_hi[4];
 };
 
@@ -222,6 +222,7 @@ struct DScene {
 #define RS_LTOP 85
 #endif
 constexpr int kLTop = RS_LTOP;
+
 
 struct DCamera {   // camera.rs:18-31
     double origin[3], lb[3], hf[3], vf[3], hu[3], vu[3];
