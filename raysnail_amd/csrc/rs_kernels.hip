@@ -1419,6 +1419,9 @@ constexpr int kClsLight = 6;
 // 7.58 -> 7.31 ms. Its camera part keeps 4 (13 VGPRs would spill).
 constexpr int ext_min_waves(int sm, bool lobj = false, int part = kExtAll) {
     if (sm == kSmSpheres && part == kExtCarried) return 5;
+#ifdef RS_N2_EXT_W2  // dev A/B: the nest-2 LDS-image extend at 2 waves (no scratch)
+    if (sm == kSmNest2 && lobj) return 2;
+#endif
     return sm == kSmNest2 ? (lobj ? 3 : 2) : 4;
 }
 
@@ -1719,7 +1722,12 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // PS: the classes of this launch -- 0 all; 1 the lean ones (Lambertian, Metal, Dielectric: bounded to 4 waves);
 // 2 the heavy ones (DiffuseMetal's two ONBs and ReflectionPdf loop, the generic switch): rs_scene::shade_split
 template <int SM, bool G4, bool LOBJ, int PS>
-__global__ __launch_bounds__(kBlock, PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
+#ifdef RS_N2_HEAVY_W2  // dev A/B: the nest-2 heavy shading (class 4 with the LDS image) at 2 waves (no scratch)
+#define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : (SM == kSmNest2 && G4 && PS == 2) ? 2 : 3)
+#else
+#define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3)
+#endif
+__global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth, uint64_t ring,
