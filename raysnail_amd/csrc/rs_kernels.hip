@@ -1412,16 +1412,14 @@ constexpr int kClsLight = 6;
 // waves/SIMD the extend is bounded to: spheres and nest-0 scenes 4 (128 VGPRs; the spheres-mode
 // camera-ray extend 144 -> 128 VGPRs: bench frame 7.86 -> 7.63 ms; nest-0 129 -> 128: example.sdl
 // 10.8 -> 10.3 ms; 5 waves spills and measured slower); nest-2 with the LDS image 3 (168 VGPRs, 184 B
-// of scratch: 4 % faster than 2 waves, 4 waves 12 % slower; profiles/r4/ab/nest2_registers), nest-2
+// of scratch: 4 % faster than 2 waves, 4 waves 12 % slower; profiles/r4/ab/nest2_registers; round 5 on the
+// C4-shaped frame: 2 waves 5.43 -> 4.54 Gseg/s, profiles/r5/ab/c4_waves_r5l), nest-2
 // with its tables in global memory 2 (its loads are L1 / L2 round trips that the spills would join)
 // The spheres mode's carried-path part (the divergent bounce >= 1 rays: lane efficiency 0.51 for BSDF rays,
 // profiles/r5/iters) at 5 waves: 96 VGPRs, 12 B of scratch, 5 blocks of 24 KiB stacks per CU; bench frame
 // 7.58 -> 7.31 ms. Its camera part keeps 4 (13 VGPRs would spill).
 constexpr int ext_min_waves(int sm, bool lobj = false, int part = kExtAll) {
     if (sm == kSmSpheres && part == kExtCarried) return 5;
-#ifdef RS_N2_EXT_W2  // dev A/B: the nest-2 LDS-image extend at 2 waves (no scratch)
-    if (sm == kSmNest2 && lobj) return 2;
-#endif
     return sm == kSmNest2 ? (lobj ? 3 : 2) : 4;
 }
 
@@ -1718,15 +1716,12 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // G4: the scene has class-4 prims (the generic material switch, composite objects), compiled in only
 // then (it sets the kernel's register count). LOBJ: the scene's tables from its LDS image (lds_scene).
 // Waves: 3; nest-2 with class 4 and the tables in global memory 1 (bounded to 3 it spilled and lost
-// 21 % on C4 in round 3; with the LDS image 3 waves measured 5 % faster than 2: nest2_registers)
+// 21 % on C4 in round 3; with the LDS image 3 waves measured 5 % faster than 2: nest2_registers; the heavy
+// launch alone at 2 waves: C4 5.43 -> 5.38 Gseg/s, profiles/r5/ab/c4_waves_r5l)
 // PS: the classes of this launch -- 0 all; 1 the lean ones (Lambertian, Metal, Dielectric: bounded to 4 waves);
 // 2 the heavy ones (DiffuseMetal's two ONBs and ReflectionPdf loop, the generic switch): rs_scene::shade_split
 template <int SM, bool G4, bool LOBJ, int PS>
-#ifdef RS_N2_HEAVY_W2  // dev A/B: the nest-2 heavy shading (class 4 with the LDS image) at 2 waves (no scratch)
-#define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : (SM == kSmNest2 && G4 && PS == 2) ? 2 : 3)
-#else
 #define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3)
-#endif
 __global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
