@@ -1373,6 +1373,7 @@ void carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
         uint32_t* qp[kWfsClasses];
         for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p = al(p + sizeof(uint32_t) * c); }
         L.d_qptrs[l] = (uint32_t**)p;
+        w.fetch = (uint32_t*)al(p + sizeof(qp));  // 1 KiB (kFetchCounters x kFetchStride words), zeroed by k_wf_gen
         if (fresh) HIP_OK(hipMemcpy(L.d_qptrs[l], qp, sizeof(qp), hipMemcpyHostToDevice));
         for (int k = 0; k < kWfsClasses; ++k) L.qptr[l][k] = qp[k];
         w.counts = nullptr;
@@ -1906,9 +1907,11 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                         // spills its stack to HBM (the overflow array is sized for that grid; a grid of resident
                         // blocks only, grid-striding, made the C5 extend 35 % slower); the rich mode a bounded grid
                         const uint32_t bn = (n + kBlock - 1) / kBlock;
-                        HIP_OK(launch_wf_extend(ds, WS, b,
-                                                sm == kSmFlat ? (ext_spill ? std::min(wide, bn) : bn) : std::min(ext_blocks, bn),
-                                                sm, cs));
+                        // flat scenes on the 4-wide tree: the persistent extend (k_wf_extend_dyn), one resident grid
+                        const uint32_t eb = sm == kSmFlat ? (flat_dyn(ds) ? std::min(ext_blocks, bn)
+                                                                          : ext_spill ? std::min(wide, bn) : bn)
+                                                          : std::min(ext_blocks, bn);
+                        HIP_OK(launch_wf_extend(ds, WS, b, eb, sm, cs));
                         if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
                         ++ki;
                         HIP_OK(launch_wf_shade(ds, WS, b, D, pp.n_items, L.d_rad,

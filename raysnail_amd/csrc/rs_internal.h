@@ -51,6 +51,13 @@ struct SceneRef {
     const DScene* host;
     const DScene* dev;
 };
+// flat scenes on the 4-wide tree: the persistent extend with lane refill (k_wf_extend_dyn; RS_NO_FLAT_DYN: the
+// one-ray-per-lane k_wf_extend, for A/B)
+#if defined(RS_NO_FLAT_DYN) || defined(RS_TRAV_STATS)
+inline bool flat_dyn(const SceneRef&) { return false; }
+#else
+inline bool flat_dyn(const SceneRef& s) { return s.host->root4 >= 0; }
+#endif
 
 // The frame's camera-sample lattice: item = sample * n_pix_local + lattice pixel (painter.rs:154-187
 // per pixel, render_rows' row interleave painter.rs:248 per lattice row).
@@ -86,6 +93,7 @@ struct WfState {
     WfSet set[2];
     double2* hit;         // per slot of the current set: (prim as bits, accepted range end)
     uint32_t* counts;     // counter block per launch step (stride kWfsStride / 1 words)
+    uint32_t* fetch;      // k_wf_extend_dyn's chunk counters (flat scenes)
     uint32_t cap;         // records per set (the sorted path fills a set from both ends)
 };
 

@@ -238,6 +238,17 @@ __device__ __forceinline__ RayC ray_consts(const Ray& r) {
     c.a = len2(r.d);
     return c;
 }
+// The same constants computed where this is called: the direction goes through an empty asm first, so
+// the compiler cannot merge two branches' copies and hoist the three f64 divisions above the branch
+// (the flat leaf test needs them only for an accepted triangle; hoisted, they ran before every leaf's loads)
+__device__ __forceinline__ RayC ray_consts_here(const Ray& r) {
+    V3 d = r.d;
+    asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));
+    RayC c;
+    c.inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    c.a = len2(d);
+    return c;
+}
 
 // A sphere record through global loads; the speed only in scenes with moving spheres
 // (DScene::moving: static spheres skip c + v*t, which is c bit for bit for v = 0)
@@ -273,6 +284,10 @@ __device__ __forceinline__ LTri ld_ltri(const LTri* arr, int i) {
     const uint32_t o = (uint32_t)i * (uint32_t)sizeof(LTri);
     const d2v a = gld<d2v>(arr, o), b = gld<d2v>(arr, o + 16), c = gld<d2v>(arr, o + 32), d = gld<d2v>(arr, o + 48),
               f = gld<d2v>(arr, o + 64);
+    // all five in registers here: the callers branch on `kind` (the last 16 B) first, and the compiler
+    // would otherwise sink the other four loads into the triangle branch -- a second dependent L2 round
+    // trip per leaf test
+    asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(d), "v"(f));
     LTri T;
     T.p0[0] = a.x; T.p0[1] = a.y; T.p0[2] = b.x; T.a = b.y; T.b = c.x; T.c = c.y; T.d = d.x; T.e = d.y; T.f = f.x;
     T.kind = f.y;
@@ -340,7 +355,7 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, 
             if (!tri_t(T, r, tmin, best, t)) return;
             // the ray constants are recomputed here (accepted triangles only) instead of being kept
             // live through the traversal: flat-scene extend runs at 5 waves on a 96-VGPR budget
-            const RayC lc = ray_consts(r);
+            const RayC lc = ray_consts_here(r);
             const DBox64& B = S.pbox[S.lprim[e]];
             if (!slab64(B.lo, B.hi, r.o, lc.inv, tmin, best)) return;
             bend = best; best = t; bp = e;
@@ -348,7 +363,7 @@ __device__ __forceinline__ void test_leaf(const DScene& S, int e, const Ray& r, 
         }
         const int p = S.lprim[e];
         const DPrim P = S.prims[p];
-        const RayC lc = ray_consts(r);
+        const RayC lc = ray_consts_here(r);
         if (P.kind == PK_SPHERE) {
             test_sphere_leaf(S, S.spheres[P.idx], e, r, lc, tmin, best, bend, bp);
         } else {
@@ -1300,9 +1315,16 @@ __device__ __forceinline__ void inj_sample(const InjParams& I, const PathParams&
     g = g0 + perm;
 }
 
+// k_wf_extend_dyn's chunk counters (WfState::fetch): zeroed by one thread of the launch before it
+constexpr uint32_t kFetchCounters = 8, kFetchStride = 32;  // counters, words apart
+__device__ __forceinline__ void zero_fetch(const WfState& W) {
+    if (blockIdx.x == 0 && threadIdx.x < kFetchCounters) W.fetch[threadIdx.x * kFetchStride] = 0u;
+}
+
 #if RS_TU_COMMON
 __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfState W, uint64_t item0, uint32_t n,
                                                    double* __restrict__ rad) {
+    zero_fetch(W);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     bool live = false;
     Ray r;
@@ -1355,10 +1377,109 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? kWfExtFlatWaves : 1) void k
     }
 }
 
+// Flat scenes (meshes), persistent extend with lane refill. In k_wf_extend a wave lives as long as its
+// slowest lane: on the C5 mesh a ray takes 18.6 node steps on average against a wave maximum of 41 (lane
+// efficiency 0.45, profiles/r5/iters/trav_stats_r5c.txt). Here a lane whose ray is done takes the next
+// one. Wave w of the grid starts on rays [64w, 64w + 64); later chunks of 64 come from one of 8 counters
+// (W.fetch, 128 B apart; counter k, taken by blockIdx % 8 -- one per XCD under round-robin dispatch, a
+// speed choice only -- hands out chunks W0 + k + 8j, W0 = the grid's waves; an empty counter sends the
+// wave to the next one). The wave refills its idle lanes, from its pool of drawn indices, once
+// RS_REFILL of them are idle (C5-shaped frame, extend per frame: 16 -> 83.8 ms, 32 -> 82.1, 48 +2 %,
+// one ray per lane (k_wf_extend) 97.2; profiles/r5/ab/c5_dyn_r5*.jsonl). Each ray's walk is
+// traverse_flat_q's (the same passes, a lane's own leaf FIFO and stack column), so its hit does not
+// depend on its lane, wave or refill time. The counters are zeroed by the launch before (k_wf_gen,
+// k_wf_shade) on the same stream.
+#ifndef RS_REFILL
+#define RS_REFILL 32
+#endif
+template <int SM>
+__global__ __launch_bounds__(kBlock, kWfExtFlatWaves) void k_wf_extend_dyn(const DScene* __restrict__ Sp, WfState W,
+                                                                            uint32_t bounce) {
+    const DScene& S = *Sp;
+    __shared__ int stk_all[stack_lds(SM) * kBlock];
+    const StkT<true, stack_lds(SM)> stk = make_stk<true, stack_lds(SM)>(S, stk_all);
+    __shared__ int leafq[RS_LEAFQ * kBlock];
+    int* const q = leafq + threadIdx.x;
+    const uint32_t n = W.counts[bounce];
+    const WfSet& cur = W.set[bounce & 1];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint32_t n_chunks = (n + 63u) >> 6;
+    const uint32_t w0 = gridDim.x * (kBlock / 64u);
+    constexpr double tmin = 0.0001;
+    const float tmin32 = -round_up_f(-tmin);
+    // the wave's pool of drawn ray indices [pa, pa + pn) (wave-uniform), its counter, counters found empty
+    uint32_t pa = (blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6)) * 64u;
+    uint32_t pn = pa < n ? min(64u, n - pa) : 0u;
+    uint32_t ck = blockIdx.x % kFetchCounters, tries = 0;
+    int i = -1, bp = -1, node = -1, sp = 0, qh = 0, qt = 0;
+    Ray r;
+    r.o = r.d = v3(0.0, 0.0, 0.0);
+    r.time = 0.0;
+    RayF4 rq = make_rayf4(make_rayf(r.o, r.o));
+    double best = RS_INF, bend = RS_INF;
+    float best32 = __builtin_huge_valf();
+    while (true) {
+        const bool idle = node < 0 && qt == qh;
+        if (idle && i >= 0) {
+            W.hit[i] = make_double2(__longlong_as_double((long long)((bp >= 0 && S.lprim) ? S.lprim[bp] : bp)), bend);
+            i = -1;
+        }
+        const uint64_t im = __ballot(idle);
+        const uint32_t ni = (uint32_t)__popcll(im);
+        if (ni >= RS_REFILL && (pn > 0 || tries < kFetchCounters)) {
+            uint32_t pb = 0, pbn = 0;  // a chunk drawn when the pool cannot serve every idle lane
+            while (pn < ni && tries < kFetchCounters) {
+                const uint32_t c0 = w0 + ck;  // counter ck's first chunk
+                if (c0 < n_chunks) {
+                    uint32_t c = 0;
+                    if (lane == 0) c = atomicAdd(W.fetch + ck * kFetchStride, 1u);
+                    c = c0 + kFetchCounters * (uint32_t)__shfl((int)c, 0);
+                    if (c < n_chunks) { pb = c * 64u; pbn = min(64u, n - pb); break; }
+                }
+                ck = (ck + 1) % kFetchCounters;
+                ++tries;
+            }
+            if (idle) {
+                const uint32_t k = (uint32_t)__popcll(im & below);
+                uint32_t j = UINT32_MAX;
+                if (k < pn) j = pa + k;
+                else if (k - pn < pbn) j = pb + (k - pn);
+                if (j != UINT32_MAX) {
+                    i = (int)j;
+                    r = load_ray(cur, j);
+                    rq = make_rayf4(make_rayf(r.o, v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z)));
+                    best = RS_INF; bend = RS_INF; best32 = __builtin_huge_valf();
+                    bp = -1; node = S.root4; sp = 0; qh = 0; qt = 0;
+                }
+            }
+            if (ni <= pn) { pa += ni; pn -= ni; }
+            else { const uint32_t u = min(ni - pn, pbn); pa = pb + u; pn = pbn - u; }
+        }
+        const bool has_leaf = qt != qh;
+        const bool can_node = node >= 0 && qt - qh <= RS_LEAFQ - 4;
+        const uint64_t work = __ballot(node >= 0 || has_leaf);
+        if (work == 0ull) break;  // every lane idle after a refill attempt: pool and counters are empty
+        const uint64_t lm = __ballot(has_leaf);
+        if (__popcll(lm) * 64 >= RS_LEAFQ_THR * __popcll(work) || __ballot(can_node) == 0ull) {
+            if (has_leaf) {
+                const int code = q[(qh & (RS_LEAFQ - 1)) * kBlock];
+                ++qh;
+                const int bp_prev = bp;
+                test_leaf<SM>(S, ~code, r, ray_consts(r), tmin, best, bend, bp);
+                if (bp != bp_prev || bp >= 0) best32 = round_up_f(best);
+            }
+        } else if (can_node) {
+            node = bvh4_node_q<SM>(S, rq, tmin32, best32, node, sp, stk, q, qt);
+        }
+    }
+}
+
 template <int SM>
 __global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ Sp, WfState W, uint32_t bounce, uint32_t depth,
                                                     uint64_t n_items, double* __restrict__ rad) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
+    zero_fetch(W);          // for the next bounce's extend (this bounce's is done: same stream)
     const uint32_t n = W.counts[bounce];
     const WfSet& cur = W.set[bounce & 1];
     const WfSet& nxt = W.set[(bounce + 1) & 1];
@@ -1980,6 +2101,12 @@ hipError_t path_mega_sm(const SceneRef& s, const DCamera& c, const PathParams& p
 
 template <int SMC>
 hipError_t wf_extend_sm(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t blocks, hipStream_t st) {
+    if constexpr (SMC == kSmFlat) {
+        if (flat_dyn(s)) {
+            hipLaunchKernelGGL(k_wf_extend_dyn<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(k_wf_extend<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce);
     return hipGetLastError();
 }
@@ -1993,7 +2120,9 @@ hipError_t wf_shade_sm(const SceneRef& s, const WfState& w, uint32_t bounce, uin
 
 template <int SMC>
 hipError_t wf_occupancy_sm(int* e, int* sh) {
-    hipError_t r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, reinterpret_cast<const void*>(&k_wf_extend<SMC>), kBlock, 0);
+    const void* ext = reinterpret_cast<const void*>(&k_wf_extend<SMC>);
+    if constexpr (SMC == kSmFlat) ext = reinterpret_cast<const void*>(&k_wf_extend_dyn<SMC>);
+    hipError_t r = hipOccupancyMaxActiveBlocksPerMultiprocessor(e, ext, kBlock, 0);
     if (r == hipSuccess)
         r = hipOccupancyMaxActiveBlocksPerMultiprocessor(sh, reinterpret_cast<const void*>(&k_wf_shade<SMC>), kBlock, 0);
     return r;

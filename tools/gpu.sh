@@ -50,8 +50,14 @@ for s in "$@"; do
     # L1 (TCP) tag accesses and misses to L2 with their latency, L2 hits / misses: the traversal's data
     # locality on the bench frame (one pass: 4 TCP + 2 TCC counters)
     (cd /tmp && step 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/l1 -o l1 -- python3 $R/tools/render_once.py 0 2 > $OUT/l1.log 2>&1) || { echo "l1 pass failed"; tail -5 $OUT/l1.log; exit 1; } ;;
+  l1mesh)
+    # the same L1 / L2 pass over two C5-shaped mesh frames (16 spp, depth 50), plus the box's counter list
+    (cd /tmp && timeout -s KILL 90 rocprofv3 -L > $OUT/counters.txt 2>&1) || echo "counter list failed (ignored)"
+    (cd /tmp && step 180 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/l1m -o l1 -- python3 $R/tools/render_once.py 0 2 mesh_scene 16 50 > $OUT/l1m.log 2>&1) || { echo "l1 mesh pass failed"; tail -5 $OUT/l1m.log; exit 1; } ;;
   mix)
-    for sc in "rtow 64 8" "quadric_sdl 16 50" "mesh_scene 16 50"; do
+    # MIXSCENES="name spp depth;...": the scenes (default the bench frame, C4's and C5's)
+    IFS=';' read -ra MSC <<< "${MIXSCENES:-rtow 64 8;quadric_sdl 16 50;mesh_scene 16 50}"
+    for sc in "${MSC[@]}"; do
       set -- $sc
       (cd $R && bash tools/pmc_mix.sh $OUT/mix_$1 - $1 $2 $3 > $OUT/mix_$1.log 2>&1) || { echo "pmc mix $1 failed"; tail -5 $OUT/mix_$1.log; exit 1; }
       (cd /tmp && step 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/mixtr_$1 -o tr -- python3 $R/tools/render_once.py 0 2 $1 $2 $3 > $OUT/mixtr_$1.log 2>&1) || { echo "mix trace $1 failed"; exit 1; }
@@ -107,6 +113,16 @@ for s in "$@"; do
       (cd $R && step 300 python3 tools/time_scene.py $v quadric 64 50 1024x1024 >> $OUT/c4.jsonl 2>> $OUT/c4.err) || { echo "c4 $v failed"; tail -5 $OUT/c4.err; exit 1; }
       echo "c4: $(tail -1 $OUT/c4.jsonl)"
     done ;;
+  c5)
+    # C5-shaped frames (the 72k-triangle mesh scene 1920x1080, 16 spp, depth 50) with the product and every variant
+    for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      [ -e "$v" ] || continue
+      (cd $R && step 300 python3 tools/time_scene.py $v mesh 16 50 1920x1080 >> $OUT/c5.jsonl 2>> $OUT/c5.err) || { echo "c5 $v failed"; tail -5 $OUT/c5.err; exit 1; }
+      echo "c5: $(tail -1 $OUT/c5.jsonl)"
+    done ;;
+  meshtests)
+    (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
+    tail -1 $OUT/pytest_mesh.log ;;
   finish)
     # depth-50 frames with the dev library at several finish points (RS_FINISH_AFTER: wavefront iterations after the
     # last injection before k_wfs_finish; 0 = none): C2, a C3-shaped RTIOW frame, C4-shaped quadric frames
