@@ -1069,6 +1069,8 @@ void build(rs_scene* s) {
         pclass[h] = (uint8_t)class_of((uint32_t)h);
         if (pclass[h] < kWfsClasses) s->class_mask |= 1u << pclass[h];
     }
+    d.lamb_only = 1;
+    for (size_t h = 0; h < s->objs.size(); ++h) d.lamb_only &= (int32_t)(pclass[h] == 0 || pclass[h] == 6);
     stage(s, d.nodes, dnodes);
     stage(s, d.pbox, pboxes);
     stage(s, d.pclass, pclass);
@@ -1374,6 +1376,7 @@ void carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
         for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p = al(p + sizeof(uint32_t) * c); }
         L.d_qptrs[l] = (uint32_t**)p;
         w.fetch = (uint32_t*)al(p + sizeof(qp));  // 1 KiB (kFetchCounters x kFetchStride words), zeroed by k_wf_gen
+        w.heads = w.fetch + 256;                   // 2 KiB: 2 banks x 8 shards x 32 words
         if (fresh) HIP_OK(hipMemcpy(L.d_qptrs[l], qp, sizeof(qp), hipMemcpyHostToDevice));
         for (int k = 0; k < kWfsClasses; ++k) L.qptr[l][k] = qp[k];
         w.counts = nullptr;
@@ -1899,6 +1902,8 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                     WfState WS = L.lane_ws[lane];
                     WS.counts = L.d_counts + chunk_i * (D + 1);
                     const hipStream_t cs = ls[lane];
+                    // a pixel mask: k_wf_gen compacts the live samples into set 0's shards (counts from zero)
+                    if (pp.mask) HIP_OK(hipMemsetAsync(WS.heads, 0, 8 * 32 * sizeof(uint32_t), cs));
                     HIP_OK(launch_wf_gen(dc, pp, WS, c0, n, L.d_rad, cs));
                     ++path_launches;
                     for (uint32_t b = 0; b < D; ++b) {
@@ -1994,6 +1999,14 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         // (2 x 32 B records) and writes a hit (16 B) per segment
         for (uint64_t c = 0; c < P.n_chunks_total; ++c)
             for (uint32_t b = 0; b < P.depth; ++b) seg += P.qc[c * (P.depth + 1) + b];
+#ifdef RS_DEV_KNOBS
+        if (s->dump_iters)
+            for (uint32_t b = 0; b < P.depth; ++b) {
+                uint64_t nb = 0;
+                for (uint64_t c = 0; c < P.n_chunks_total; ++c) nb += P.qc[c * (P.depth + 1) + b];
+                std::fprintf(stderr, "bounce %2u: %11llu paths\n", b, (unsigned long long)nb);
+            }
+#endif
         stats->kernel_id = RS_KERNEL_WF_EXTEND;
         kbytes = 80ull * seg;
     } else {

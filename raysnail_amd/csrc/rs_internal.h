@@ -58,6 +58,13 @@ inline bool flat_dyn(const SceneRef&) { return false; }
 #else
 inline bool flat_dyn(const SceneRef& s) { return s.host->root4 >= 0; }
 #endif
+// flat scenes whose shading is Lambertian / DiffuseLight only: k_wf_shade<kSmFlat, true> (RS_NO_FLAT_LAMB: the
+// generic one, for A/B)
+#ifdef RS_NO_FLAT_LAMB
+inline bool flat_lamb(const SceneRef&) { return false; }
+#else
+inline bool flat_lamb(const SceneRef& s) { return s.host->lamb_only != 0; }
+#endif
 
 // The frame's camera-sample lattice: item = sample * n_pix_local + lattice pixel (painter.rs:154-187
 // per pixel, render_rows' row interleave painter.rs:248 per lattice row).
@@ -94,6 +101,7 @@ struct WfState {
     double2* hit;         // per slot of the current set: (prim as bits, accepted range end)
     uint32_t* counts;     // counter block per launch step (stride kWfsStride / 1 words)
     uint32_t* fetch;      // k_wf_extend_dyn's chunk counters (flat scenes)
+    uint32_t* heads;      // bounce-synchronous sets: 2 banks x 8 shards x (count, region offset) (rs_kernels.hip Segs)
     uint32_t cap;         // records per set (the sorted path fills a set from both ends)
 };
 

@@ -1040,7 +1040,9 @@ __device__ __forceinline__ V3 emission(const DScene& S, const DMaterial& M0, con
 // One level of TakePhotoSettings::ray_color (camera.rs:156-255) after world.hit: adds this
 // level's contribution to L and, when the recursion continues, replaces `ray` and multiplies the
 // path throughput T by this level's factor. Returns true when the path continues.
-template <int SM>
+// KIND = RS_MAT_LAMBERTIAN: the scene's hits carry Lambertian or DiffuseLight materials only (DScene::lamb_only),
+// so no MixedMaterial resolution and the Lambertian scatter alone
+template <int SM, int KIND = -1>
 __device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray, V3& T, V3& L, Rng& rng) {
     if (!hit_ok) {  // camera.rs:253-254 background
         V3 bg = background(S, ray);
@@ -1052,6 +1054,11 @@ __device__ bool shade_step(const DScene& S, bool hit_ok, const Hit& h, Ray& ray,
     if (M0.kind == RS_MAT_DIFFUSE_LIGHT) {  // scatter None -> emitted
         V3 e = emission<rich_of(SM)>(S, M0, h);
         L = L + v3(T.x * e.x, T.y * e.y, T.z * e.z);
+        return false;
+    }
+    if constexpr (KIND == RS_MAT_LAMBERTIAN) {
+        if (shade_surface<RS_MAT_LAMBERTIAN, SM>(S, h, M0, M0, ray, T, rng)) return true;
+        L = close_path(L, T);
         return false;
     }
     int ms = mi;
@@ -1321,7 +1328,74 @@ __device__ __forceinline__ void zero_fetch(const WfState& W) {
     if (blockIdx.x == 0 && threadIdx.x < kFetchCounters) W.fetch[threadIdx.x * kFetchStride] = 0u;
 }
 
+// ---- sharded path sets of the bounce-synchronous wavefront ----
+// A launch that compacts its survivors into the next set does it per block: one returning atomic per
+// block on a count. On one word that saturates at ~88 atomics/us (MI355X_MICROARCH.md, 'dequeue') and its
+// latency grows with the blocks waiting on it: with the mesh shading at 4 waves the bounce-0 launch took
+// 2.54 ms, 1.56 ms with the same atomics spread over 8 words (profiles/r5/ab/c5_slot_spread_r5s.txt). So a
+// set is kShards shards: input tile t (kBlock items of the producer's input, in its virtual order) sends
+// its survivors to shard t % kShards, whose region has room for every item of its tiles (shard_cap); a
+// shard's survivors are compacted at the start of its region. WfState::heads holds two banks (set b in bank
+// b & 1) of kShards (count, region offset) pairs on their own 128-byte lines. A consumer walks the set in
+// virtual order (shard 0's survivors, then shard 1's, ...: seg_pos). The extend of bounce b publishes the
+// set's size in counts[b] (the host's statistics) and zeroes the other bank's counts for the shading of b.
+constexpr uint32_t kShards = 8, kShardStride = 32;  // shards, words apart
+__device__ __forceinline__ uint32_t* shard_bank(const WfState& W, uint32_t b) {
+    return W.heads + (b & 1u) * (kShards * kShardStride);
+}
+struct Segs {
+    uint32_t cnt[kShards], off[kShards];
+    uint32_t n;
+};
+__device__ __forceinline__ Segs load_segs(const WfState& W, uint32_t b) {
+    const uint32_t* h = shard_bank(W, b);
+    Segs g;
+    g.n = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kShards; ++k) {
+        g.cnt[k] = h[k * kShardStride];
+        g.off[k] = h[k * kShardStride + 1];
+        g.n += g.cnt[k];
+    }
+    return g;
+}
+// virtual index v (< g.n) -> the record's position
+__device__ __forceinline__ uint32_t seg_pos(const Segs& g, uint32_t v) {
+    uint32_t pos = 0, pre = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kShards; ++k) {
+        if (v >= pre && v - pre < g.cnt[k]) pos = g.off[k] + (v - pre);
+        pre += g.cnt[k];
+    }
+    return pos;
+}
+// items of shard h's tiles for an input of n items (tile t = items [t * kBlock, (t + 1) * kBlock) -> shard t % kShards)
+__device__ __forceinline__ uint32_t shard_cap(uint32_t n, uint32_t h) {
+    const uint32_t F = n / kBlock, rem = n % kBlock;
+    const uint32_t full = F > h ? (F - h + kShards - 1) / kShards : 0u;
+    return full * kBlock + (F % kShards == h ? rem : 0u);
+}
+__device__ __forceinline__ uint32_t shard_off(uint32_t n, uint32_t h) {
+    uint32_t o = 0;
+    for (uint32_t j = 0; j < h; ++j) o += shard_cap(n, j);
+    return o;
+}
+// the producer of bank b's set, input of n items: the shards' region offsets (block 0)
+__device__ __forceinline__ void publish_offsets(const WfState& W, uint32_t b, uint32_t n) {
+    if (blockIdx.x == 0 && threadIdx.x < kShards) shard_bank(W, b)[threadIdx.x * kShardStride + 1] = shard_off(n, threadIdx.x);
+}
+// the consumer of set b (the extend): its size for the host, and the other bank's counts zeroed for the
+// shading's survivors (that bank's set, b - 1, is done with)
+__device__ __forceinline__ void extend_prologue(const WfState& W, uint32_t b, uint32_t n) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) W.counts[b] = n;
+        if (threadIdx.x < kShards) shard_bank(W, b + 1)[threadIdx.x * kShardStride] = 0u;
+    }
+}
+
 #if RS_TU_COMMON
+// The chunk's camera samples (set 0). Without a pixel mask every sample is live and record i is item i
+// (one shard holding all n); with one, the live samples are compacted into shards (counts zeroed by the host).
 __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfState W, uint64_t item0, uint32_t n,
                                                    double* __restrict__ rad) {
     zero_fetch(W);
@@ -1336,14 +1410,21 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
         if (!live) put_rad(rad, item, 0.0, 0.0, 0.0);
     }
     if (!P.mask && P.depth > 0) {
-        // no pixel mask: every camera sample is live, so record i is thread i's (no compaction, and
-        // no returning atomic per block on one word -- ~88/us, which bounded this kernel)
-        if (i == 0) W.counts[0] = n;
+        // eight contiguous shards of whole 64-record chunks (the extend's waves draw from all eight counters)
+        if (blockIdx.x == 0 && threadIdx.x < kShards) {
+            uint32_t* const h = shard_bank(W, 0) + threadIdx.x * kShardStride;
+            const uint32_t step = ((n + kShards - 1) / kShards + 63u) & ~63u;
+            const uint32_t a = min(n, threadIdx.x * step), b = min(n, a + step);
+            h[0] = b - a;
+            h[1] = a;
+        }
         if (live) store_path(W.set[0], i, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
         return;
     }
-    const uint32_t slot = block_slot1(live, &W.counts[0]);
-    if (live) store_path(W.set[0], slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
+    publish_offsets(W, 0, n);
+    const uint32_t sh = blockIdx.x % kShards;
+    const uint32_t slot = block_slot1(live, shard_bank(W, 0) + sh * kShardStride);
+    if (live) store_path(W.set[0], shard_off(n, sh) + slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
 }
 #endif  // RS_TU_COMMON
 
@@ -1356,11 +1437,14 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? kWfExtFlatWaves : 1) void k
     __shared__ int stk_all[stack_lds(SM) * kBlock];
     const StkT<true, stack_lds(SM)> stk = make_stk<true, stack_lds(SM)>(S, stk_all);
     __shared__ int leafq[SM == kSmFlat ? RS_LEAFQ * kBlock : 1];
-    const uint32_t n = W.counts[bounce];
+    const Segs in = load_segs(W, bounce);
+    const uint32_t n = in.n;
+    extend_prologue(W, bounce, n);
     const WfSet& cur = W.set[bounce & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        const uint32_t i = base + threadIdx.x;
-        if (i < n) {
+        const uint32_t v = base + threadIdx.x;
+        if (v < n) {
+            const uint32_t i = seg_pos(in, v);
             Ray r = load_ray(cur, i);
             if (rich_of(SM) && S.has_media) r.key = load_rng(cur, i).medium_key();  // the segment's medium key
             double bend = RS_INF;
@@ -1372,7 +1456,7 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? kWfExtFlatWaves : 1) void k
             W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
         }
 #ifdef RS_TRAV_STATS
-        trav_stats_flush(i < n);
+        trav_stats_flush(v < n);
 #endif
     }
 }
@@ -1380,14 +1464,13 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? kWfExtFlatWaves : 1) void k
 // Flat scenes (meshes), persistent extend with lane refill. In k_wf_extend a wave lives as long as its
 // slowest lane: on the C5 mesh a ray takes 18.6 node steps on average against a wave maximum of 41 (lane
 // efficiency 0.45, profiles/r5/iters/trav_stats_r5c.txt). Here a lane whose ray is done takes the next
-// one. Wave w of the grid starts on rays [64w, 64w + 64); later chunks of 64 come from one of 8 counters
-// (W.fetch, 128 B apart; counter k, taken by blockIdx % 8 -- one per XCD under round-robin dispatch, a
-// speed choice only -- hands out chunks W0 + k + 8j, W0 = the grid's waves; an empty counter sends the
-// wave to the next one). The wave refills its idle lanes, from its pool of drawn indices, once
-// RS_REFILL of them are idle (C5-shaped frame, extend per frame: 16 -> 83.8 ms, 32 -> 82.1, 48 +2 %,
-// one ray per lane (k_wf_extend) 97.2; profiles/r5/ab/c5_dyn_r5*.jsonl). Each ray's walk is
-// traverse_flat_q's (the same passes, a lane's own leaf FIFO and stack column), so its hit does not
-// depend on its lane, wave or refill time. The counters are zeroed by the launch before (k_wf_gen,
+// one. A wave draws chunks of 64 records of one shard of the set from that shard's counter (W.fetch, 128 B
+// apart; the wave starts on shard blockIdx % 8 -- one per XCD under round-robin dispatch, a speed choice
+// only -- and moves to the next shard when its shard is empty), and refills its idle lanes from its pool
+// of drawn records once RS_REFILL of them are idle (C5-shaped frame, extend per frame: 16 -> 83.8 ms,
+// 32 -> 82.1, 48 +2 %, one ray per lane (k_wf_extend) 97.2; profiles/r5/ab/c5_dyn_r5*.jsonl). Each ray's
+// walk is traverse_flat_q's (the same passes, a lane's own leaf FIFO and stack column), so its hit does
+// not depend on its lane, wave or refill time. The counters are zeroed by the launch before (k_wf_gen,
 // k_wf_shade) on the same stream.
 #ifndef RS_REFILL
 #define RS_REFILL 32
@@ -1400,17 +1483,15 @@ __global__ __launch_bounds__(kBlock, kWfExtFlatWaves) void k_wf_extend_dyn(const
     const StkT<true, stack_lds(SM)> stk = make_stk<true, stack_lds(SM)>(S, stk_all);
     __shared__ int leafq[RS_LEAFQ * kBlock];
     int* const q = leafq + threadIdx.x;
-    const uint32_t n = W.counts[bounce];
+    const Segs in = load_segs(W, bounce);
+    extend_prologue(W, bounce, in.n);
     const WfSet& cur = W.set[bounce & 1];
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t below = (1ull << lane) - 1ull;
-    const uint32_t n_chunks = (n + 63u) >> 6;
-    const uint32_t w0 = gridDim.x * (kBlock / 64u);
     constexpr double tmin = 0.0001;
     const float tmin32 = -round_up_f(-tmin);
-    // the wave's pool of drawn ray indices [pa, pa + pn) (wave-uniform), its counter, counters found empty
-    uint32_t pa = (blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6)) * 64u;
-    uint32_t pn = pa < n ? min(64u, n - pa) : 0u;
+    // the wave's pool of drawn records [pa, pa + pn) (wave-uniform), its shard, shards found empty
+    uint32_t pa = 0, pn = 0;
     uint32_t ck = blockIdx.x % kFetchCounters, tries = 0;
     int i = -1, bp = -1, node = -1, sp = 0, qh = 0, qt = 0;
     Ray r;
@@ -1430,12 +1511,15 @@ __global__ __launch_bounds__(kBlock, kWfExtFlatWaves) void k_wf_extend_dyn(const
         if (ni >= RS_REFILL && (pn > 0 || tries < kFetchCounters)) {
             uint32_t pb = 0, pbn = 0;  // a chunk drawn when the pool cannot serve every idle lane
             while (pn < ni && tries < kFetchCounters) {
-                const uint32_t c0 = w0 + ck;  // counter ck's first chunk
-                if (c0 < n_chunks) {
+                uint32_t cnt = 0, off = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < kShards; ++k)
+                    if (k == ck) { cnt = in.cnt[k]; off = in.off[k]; }
+                if (cnt > 0) {
                     uint32_t c = 0;
                     if (lane == 0) c = atomicAdd(W.fetch + ck * kFetchStride, 1u);
-                    c = c0 + kFetchCounters * (uint32_t)__shfl((int)c, 0);
-                    if (c < n_chunks) { pb = c * 64u; pbn = min(64u, n - pb); break; }
+                    c = (uint32_t)__shfl((int)c, 0) * 64u;
+                    if (c < cnt) { pb = off + c; pbn = min(64u, cnt - c); break; }
                 }
                 ck = (ck + 1) % kFetchCounters;
                 ++tries;
@@ -1459,7 +1543,7 @@ __global__ __launch_bounds__(kBlock, kWfExtFlatWaves) void k_wf_extend_dyn(const
         const bool has_leaf = qt != qh;
         const bool can_node = node >= 0 && qt - qh <= RS_LEAFQ - 4;
         const uint64_t work = __ballot(node >= 0 || has_leaf);
-        if (work == 0ull) break;  // every lane idle after a refill attempt: pool and counters are empty
+        if (work == 0ull) break;  // every lane idle after a refill attempt: pool and shards are empty
         const uint64_t lm = __ballot(has_leaf);
         if (__popcll(lm) * 64 >= RS_LEAFQ_THR * __popcll(work) || __ballot(can_node) == 0ull) {
             if (has_leaf) {
@@ -1475,22 +1559,32 @@ __global__ __launch_bounds__(kBlock, kWfExtFlatWaves) void k_wf_extend_dyn(const
     }
 }
 
-template <int SM>
-__global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ Sp, WfState W, uint32_t bounce, uint32_t depth,
+// LAMB: the scene's shading is Lambertian / DiffuseLight only (DScene::lamb_only), compiled for that alone
+// (C5-shaped frame, shading per frame: 18.6 ms unbounded (3 waves), 22.4 at 4 waves (36 B of scratch), the
+// generic kernel 23.5; profiles/r5/ab/c5_shards_r5t.txt)
+#ifndef RS_LAMB_WAVES
+#define RS_LAMB_WAVES 1
+#endif
+template <int SM, bool LAMB = false>
+__global__ __launch_bounds__(kBlock, LAMB ? RS_LAMB_WAVES : 1) void k_wf_shade(const DScene* __restrict__ Sp, WfState W, uint32_t bounce, uint32_t depth,
                                                     uint64_t n_items, double* __restrict__ rad) {
     const DScene& S = *Sp;  // the scene lives in device memory: no by-value copy in scratch
     zero_fetch(W);          // for the next bounce's extend (this bounce's is done: same stream)
-    const uint32_t n = W.counts[bounce];
+    const Segs in = load_segs(W, bounce);
+    const uint32_t n = in.n;
+    publish_offsets(W, bounce + 1, n);
+    uint32_t* const out = shard_bank(W, bounce + 1);
     const WfSet& cur = W.set[bounce & 1];
     const WfSet& nxt = W.set[(bounce + 1) & 1];
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = base + threadIdx.x;
         bool alive = false;
         Ray r;
         V3 T, L = v3(0.0, 0.0, 0.0);  // a live path's radiance (WfSet)
         Rng rng;
         uint32_t item = 0;
-        if (i < n) {
+        if (v < n) {
+            const uint32_t i = seg_pos(in, v);
             load_path(cur, i, r, T, rng);
             if (rich_of(SM) && S.has_media) r.key = rng.medium_key();
             const double2 hb = W.hit[i];
@@ -1498,15 +1592,16 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(const DScene* __restrict__ 
             Hit h;
             const bool ok = finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
             item = cur.tag[i].x;
-            alive = shade_step<SM>(S, ok, h, r, T, L, rng);
+            alive = shade_step<SM, LAMB ? RS_MAT_LAMBERTIAN : -1>(S, ok, h, r, T, L, rng);
             if (alive && bounce + 1 >= depth) {  // depth limit
                 L = close_path(L, T);
                 alive = false;
             }
             if (!alive) put_rad(rad, item, L.x, L.y, L.z);
         }
-        const uint32_t slot = block_slot1(alive, &W.counts[bounce + 1]);
-        if (alive) store_path(nxt, slot, r, T, rng, item);
+        const uint32_t sh = (base / kBlock) % kShards;
+        const uint32_t slot = block_slot1(alive, out + sh * kShardStride);
+        if (alive) store_path(nxt, shard_off(n, sh) + slot, r, T, rng, item);
     }
 }
 
@@ -2114,6 +2209,12 @@ hipError_t wf_extend_sm(const SceneRef& s, const WfState& w, uint32_t bounce, ui
 template <int SMC>
 hipError_t wf_shade_sm(const SceneRef& s, const WfState& w, uint32_t bounce, uint32_t depth, uint64_t n_items,
                        double* rad, uint32_t blocks, hipStream_t st) {
+    if constexpr (SMC == kSmFlat) {
+        if (flat_lamb(s)) {
+            hipLaunchKernelGGL((k_wf_shade<SMC, true>), dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, depth, n_items, rad);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(k_wf_shade<SMC>, dim3(blocks), dim3(kBlock), 0, st, s.dev, w, bounce, depth, n_items, rad);
     return hipGetLastError();
 }

@@ -212,6 +212,8 @@ struct DScene {
     int32_t moving;          // 1: some sphere has a nonzero speed (center_at needs the time)
     int32_t ltop;            // spheres mode: the first ltop nodes of nodes4 (breadth-first, root 0) are the tree's
                              // top, which the extend's blocks also hold in LDS (rs_kernels.hip s_top4); 0: none
+    int32_t lamb_only;       // 1: every prim's hits carry a Lambertian or a DiffuseLight material (shading classes
+                             // 0 and 6 only): the flat scenes' shading kernel compiled for Lambertian alone
     float bg_lo[4], bg_hi[4];
 };
 

@@ -120,6 +120,16 @@ for s in "$@"; do
       (cd $R && step 300 python3 tools/time_scene.py $v mesh 16 50 1920x1080 >> $OUT/c5.jsonl 2>> $OUT/c5.err) || { echo "c5 $v failed"; tail -5 $OUT/c5.err; exit 1; }
       echo "c5: $(tail -1 $OUT/c5.jsonl)"
     done ;;
+  c5trace)
+    # kernel traces of one C5-shaped mesh frame per library (product and variants): per-launch extend / shade times
+    for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      [ -e "$v" ] || continue
+      n=$(basename $v .so)
+      (cd /tmp && step 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/c5t_$n -o tr -- python3 $R/tools/time_scene.py $v mesh 16 50 1920x1080 > $OUT/c5t_$n.log 2>&1) || { echo "c5 trace $n failed"; tail -5 $OUT/c5t_$n.log; exit 1; }
+      echo "== $n" >> $OUT/c5trace.txt
+      (cd $R && python3 tools/launch_times.py $OUT/c5t_$n/tr_kernel_trace.csv >> $OUT/c5trace.txt)
+    done
+    cat $OUT/c5trace.txt ;;
   meshtests)
     (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
     tail -1 $OUT/pytest_mesh.log ;;
