@@ -1211,38 +1211,6 @@ __device__ __forceinline__ uint32_t block_slot(int cls, uint32_t* const* counter
     __syncthreads();  // wcnt / bbase are reused by the next call
     return slot;
 }
-// block_slot for C runs whose lanes are also ordered by a key in [0, K) inside the block's chunk of each run:
-// slots of run c are the run's block base + (key, wave, lane) order, so consecutive records of a run hold
-// rays of one key (one atomic per block and run, as block_slot).
-template <int C, int K>
-__device__ __forceinline__ uint32_t block_slot_keyed(int cls, int key, uint32_t* const* counters) {
-    __shared__ uint32_t wk[C][K][kBlock / 64];
-    __shared__ uint32_t kb[C];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long mine = 0ull;
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const bool me = cls == c && key == k;
-            const unsigned long long m = __ballot(me);
-            if (me) mine = m;
-            if (lane == 0) wk[c][k][wave] = (uint32_t)__popcll(m);
-        }
-    __syncthreads();
-    if (threadIdx.x < C) {
-        const int c = threadIdx.x;
-        uint32_t tot = 0;
-        for (int k = 0; k < K; ++k)
-            for (int w = 0; w < kBlock / 64; ++w) { const uint32_t n = wk[c][k][w]; wk[c][k][w] = tot; tot += n; }
-        kb[c] = tot ? atomicAdd(counters[c], tot) : 0u;
-    }
-    __syncthreads();
-    uint32_t slot = 0;
-    if (cls >= 0 && cls < C) slot = kb[cls] + wk[cls][key][wave] + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull));
-    __syncthreads();
-    return slot;
-}
 __device__ __forceinline__ uint32_t block_slot1(bool flag, uint32_t* counter) {
     uint32_t* const cs[1] = {counter};
     return block_slot<1>(flag ? 0 : -1, cs);
@@ -1913,12 +1881,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
     // the front, the rest from the back: the next extend's waves then trace rays of one kind
     uint32_t* const gc[2] = {&cnt_next[cix(kCntBack)], &cnt_next[cix(kCntFront)]};
-#ifdef RS_BIN_OCT  // dev A/B: the next set's runs ordered by direction octant inside each block's chunk
-    const int oct = (r.d.x < 0.0 ? 1 : 0) | (r.d.y < 0.0 ? 2 : 0) | (r.d.z < 0.0 ? 4 : 0);
-    const uint32_t slot = block_slot_keyed<2, 8>(alive ? light_ray : -1, oct, gc);
-#else
     const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
-#endif
     if (alive) {
         const uint32_t p = light_ray ? slot : W.cap - 1u - slot;
         store_path(nxt, p, r, T, rng, item, lvl + 1u);

@@ -130,6 +130,16 @@ for s in "$@"; do
       (cd $R && python3 tools/launch_times.py $OUT/c5t_$n/tr_kernel_trace.csv >> $OUT/c5trace.txt)
     done
     cat $OUT/c5trace.txt ;;
+  probe)
+    # kernel traces of one bench frame per library (product and variants): the first launches of each kernel
+    for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      [ -e "$v" ] || continue
+      n=$(basename $v .so)
+      (cd /tmp && RS_HIP_LIB=$v step 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/pr_$n -o tr -- python3 $R/tools/render_once.py 0 1 > $OUT/pr_$n.log 2>&1) || { echo "probe trace $n failed"; tail -5 $OUT/pr_$n.log; exit 1; }
+      echo "== $n" >> $OUT/probe.txt
+      (cd $R && python3 tools/launch_times.py $OUT/pr_$n/tr_kernel_trace.csv 20 first >> $OUT/probe.txt)
+    done
+    cat $OUT/probe.txt ;;
   meshtests)
     (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
     tail -1 $OUT/pytest_mesh.log ;;
