@@ -140,6 +140,10 @@ for s in "$@"; do
       (cd $R && python3 tools/launch_times.py $OUT/pr_$n/tr_kernel_trace.csv 20 first >> $OUT/probe.txt)
     done
     cat $OUT/probe.txt ;;
+  c4trace)
+    # kernel trace of C4-shaped frames (quadric.sdl + Cornell emitter 1024x1024, 256 spp, depth 50)
+    (cd /tmp && step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4t -o tr -- python3 $R/tools/time_scene.py default quadric 256 50 1024x1024 > $OUT/c4t.log 2>&1) || { echo "c4 trace failed"; tail -5 $OUT/c4t.log; exit 1; }
+    tail -1 $OUT/c4t.log ;;
   meshtests)
     (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
     tail -1 $OUT/pytest_mesh.log ;;
