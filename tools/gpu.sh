@@ -164,8 +164,13 @@ for s in "$@"; do
   iters)
     # one lane, the dev library: per-iteration queue counts (RS_DUMP_ITERS) and the carried front run / the
     # rest in separate extend launches (RS_SPLIT_RUNS) under a kernel trace; then the per-launch table
-    (cd /tmp && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_DUMP_ITERS=1 RS_SPLIT_RUNS=1 step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/iters -o it -- python3 $R/tools/render_once.py 0 4 > $OUT/iters.log 2>&1) || { echo "iters trace failed"; tail -5 $OUT/iters.log; exit 1; }
-    (cd $R && python3 tools/iter_table.py $OUT/iters.log $(ls $OUT/iters/*kernel_trace.csv) | tee $OUT/iters.txt) ;;
+    # ITERSCENES="name spp depth;...": the frames (default the bench frame and C2's example.sdl frame)
+    IFS=';' read -ra ISC <<< "${ITERSCENES:-rtow 64 8;example_sdl 64 50}"
+    for sc in "${ISC[@]}"; do
+      set -- $sc
+      (cd /tmp && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_DUMP_ITERS=1 RS_SPLIT_RUNS=1 step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/iters_$1 -o it -- python3 $R/tools/render_once.py 0 4 $1 $2 $3 > $OUT/iters_$1.log 2>&1) || { echo "iters trace $1 failed"; tail -5 $OUT/iters_$1.log; exit 1; }
+      (cd $R && python3 tools/iter_table.py $OUT/iters_$1.log $(ls $OUT/iters_$1/*kernel_trace.csv) | tee $OUT/iters_$1.txt)
+    done ;;
   configs)
     (cd $R && step 900 python3 tools/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err) || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
     cat $OUT/configs.jsonl ;;
