@@ -144,6 +144,16 @@ for s in "$@"; do
     # kernel trace of C4-shaped frames (quadric.sdl + Cornell emitter 1024x1024, 256 spp, depth 50)
     (cd /tmp && step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4t -o tr -- python3 $R/tools/time_scene.py default quadric 256 50 1024x1024 > $OUT/c4t.log 2>&1) || { echo "c4 trace failed"; tail -5 $OUT/c4t.log; exit 1; }
     tail -1 $OUT/c4t.log ;;
+  c3)
+    # C3-shaped frames (RTIOW 1920x1080, 64 spp, depth 50) with the product, every variant, and the dev library
+    # with RS_EXT_SPLIT=1 (carried part and camera part in separate launches on iterations with both)
+    for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      [ -e "$v" ] || continue
+      (cd $R && step 300 python3 tools/time_scene.py $v rtow 64 50 1920x1080 >> $OUT/c3.jsonl 2>> $OUT/c3.err) || { echo "c3 $v failed"; tail -5 $OUT/c3.err; exit 1; }
+      echo "c3: $(tail -1 $OUT/c3.jsonl)"
+    done
+    (cd $R && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_EXT_SPLIT=1 step 300 python3 tools/time_scene.py $R/raysnail_amd/lib/libraysnail_hip_dev.so rtow 64 50 1920x1080 >> $OUT/c3.jsonl 2>> $OUT/c3.err) || { echo "c3 dev split failed"; exit 1; }
+    echo "c3 dev RS_EXT_SPLIT=1: $(tail -1 $OUT/c3.jsonl)" ;;
   meshtests)
     (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
     tail -1 $OUT/pytest_mesh.log ;;
