@@ -174,6 +174,30 @@ def test_pixel_mask_and_untouched_rows(gpu):
     assert np.array_equal(out, ref)
 
 
+@pytest.mark.parametrize("name", ["mesh", "mesh_metal", "smoke"])
+def test_pixel_mask_bounce_synchronous(gpu, name):
+    """The bounce-synchronous wavefront (a flat mesh scene -- Lambertian only, k_wf_shade<kSmFlat, true>, or
+    with Metal / Dielectric spheres, the generic shading -- and a rich media scene) under a pixel mask:
+    k_wf_gen compacts the live samples into set 0's shards (rs_kernels.hip Segs); masked pixels come back 0,
+    the frame equals the oracle's and the unmasked pixels the maskless frame's."""
+    if name.startswith("mesh"):
+        cam, world = scenes.mesh_scene(48, 32, n_theta=20, n_phi=40)
+        if name == "mesh_metal":
+            from raysnail_amd.api import Color, Dielectric, Glass, Metal, Sphere
+            world.hittables.add(Sphere((1.4, 0.6, 0.3), 0.5, Metal(Color(0.7, 0.6, 0.5, 1.0))))
+            world.hittables.add(Sphere((-1.3, 0.5, 0.8), 0.45, Dielectric(Color(1.0, 1.0, 1.0, 1.0), 1.5).reflect_curve(Glass())))
+    else:
+        cam, world = scenes.cornell_smoke(48, 32)
+    photo = cam.take_photo().samples(4).depth(8).seed(5)
+    full = photo.shot(None, world)
+    mask = (np.indices((32, 48)).sum(0) % 5 != 0).astype(np.uint8)
+    out, _ = world.device_scene().render(cam.desc, photo.settings(), mask)
+    assert np.all(out[mask == 0] == 0.0)
+    assert np.array_equal(out[mask == 1], full[mask == 1])
+    ref, _ = _oracle(world).render(cam.desc, photo.settings(), threads=8, mask=mask)
+    assert np.array_equal(out, ref)
+
+
 def test_deep_paths_depth50(gpu):
     """Depth-50 recursion (configs 2-5): wavefront keeps bouncing until every queue drains."""
     for build in (lambda: scenes.rtow_13_1(40, 25)[:2], lambda: scenes.cornell_box(32, 32)):

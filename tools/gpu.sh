@@ -154,6 +154,13 @@ for s in "$@"; do
     done
     (cd $R && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_EXT_SPLIT=1 step 300 python3 tools/time_scene.py $R/raysnail_amd/lib/libraysnail_hip_dev.so rtow 64 50 1920x1080 >> $OUT/c3.jsonl 2>> $OUT/c3.err) || { echo "c3 dev split failed"; exit 1; }
     echo "c3 dev RS_EXT_SPLIT=1: $(tail -1 $OUT/c3.jsonl)" ;;
+  c2)
+    # C2-shaped frames (example.sdl 800x500, 64 spp, depth 50) with the product and every variant
+    for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      [ -e "$v" ] || continue
+      (cd $R && step 300 python3 tools/time_scene.py $v example 64 50 800x500 >> $OUT/c2.jsonl 2>> $OUT/c2.err) || { echo "c2 $v failed"; tail -5 $OUT/c2.err; exit 1; }
+      echo "c2: $(tail -1 $OUT/c2.jsonl)"
+    done ;;
   meshtests)
     (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
     tail -1 $OUT/pytest_mesh.log ;;
