@@ -1344,6 +1344,17 @@ void ensure_stack_overflow(const rs_scene* s, Replica& R, uint64_t threads) {
     R.ds.stk_ovf = R.d_ovf;
 }
 
+// a static scene's path records carry (item, level) in ray_o.w (rs_kernels.hip store_path; RS_NO_TAGW: the tag
+// array, for A/B)
+uint32_t tag_in_ray(const SceneRef& s) {
+#ifdef RS_NO_TAGW
+    (void)s;
+    return 0u;
+#else
+    return s.host->moving == 0 ? 1u : 0u;
+#endif
+}
+
 // Path state of `lanes` lanes of capacity `cap` paths per set each (L.lane_ws[l], L.d_qptrs[l], L.qptr[l]).
 void carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
     const size_t per_set = 3 * sizeof(D4) + sizeof(uint2);
@@ -1747,6 +1758,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  const LaneSched& ln = f.lane[l];
                  const hipStream_t cs = ls[l];
                  WfState WS = L.lane_ws[l];
+                 WS.tagw = tag_in_ray(ds);
                  WS.counts = L.d_counts + ln.cnt_off;
                  uint32_t** qd = L.d_qptrs[l];
                  const uint32_t n_new = ln.n_new(t);
@@ -1900,6 +1912,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                 for (uint64_t c0 = 0; c0 < pp.n_items; c0 += chunk, ++chunk_i, lane = (lane + 1) % lanes) {
                     const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, pp.n_items - c0);
                     WfState WS = L.lane_ws[lane];
+                    WS.tagw = tag_in_ray(ds);
                     WS.counts = L.d_counts + chunk_i * (D + 1);
                     const hipStream_t cs = ls[lane];
                     // a pixel mask: k_wf_gen compacts the live samples into set 0's shards (counts from zero)

@@ -103,6 +103,7 @@ struct WfState {
     uint32_t* fetch;      // k_wf_extend_dyn's chunk counters (flat scenes)
     uint32_t* heads;      // bounce-synchronous sets: 2 banks x 8 shards x (count, region offset) (rs_kernels.hip Segs)
     uint32_t cap;         // records per set (the sorted path fills a set from both ends)
+    uint32_t tagw;        // 1: no moving sphere -- (item, level) ride in ray_o.w instead of `tag` (rs_kernels.hip store_path)
 };
 
 // Streaming wavefront (k_wfs_extend): the camera samples injected by one iteration. The frame's

@@ -1164,12 +1164,19 @@ __device__ __forceinline__ void unpack_u32x2(double v, uint32_t& lo, uint32_t& h
     lo = (uint32_t)u;
     hi = (uint32_t)(u >> 32);
 }
-__device__ __forceinline__ Ray load_ray(const WfSet& W, uint32_t p) {
+// tw (WfState::tagw): the scene has no moving sphere, so a path's time is never read (a static sphere's centre
+// is c + 0 * t = c for any finite t >= 0, sphere.rs center_at), and its record carries (item, level) in ray_o.w
+// instead of the tag array: 8 B less each way per record (the shading is bound by its record traffic)
+__device__ __forceinline__ Ray load_ray(const WfSet& W, uint32_t p, bool tw = false, uint2* tag = nullptr) {
     const D4 a = W.ray_o[p], b = W.ray_d[p];
     Ray r;
-    r.o = v3(a.x, a.y, a.z); r.time = a.w;
+    r.o = v3(a.x, a.y, a.z); r.time = tw ? 0.0 : a.w;
     r.d = v3(b.x, b.y, b.z);
     r.key = 0;
+    if (tag) {
+        if (tw) unpack_u32x2(a.w, tag->x, tag->y);
+        else *tag = W.tag[p];
+    }
     return r;
 }
 __device__ __forceinline__ Rng load_rng(const WfSet& W, uint32_t p) {
@@ -1178,23 +1185,25 @@ __device__ __forceinline__ Rng load_rng(const WfSet& W, uint32_t p) {
     unpack_u32x2(W.thr[p].w, g.z, g.w);
     return g;
 }
-__device__ __forceinline__ void load_path(const WfSet& W, uint32_t p, Ray& r, V3& T, Rng& rng) {
+__device__ __forceinline__ void load_path(const WfSet& W, uint32_t p, Ray& r, V3& T, Rng& rng, bool tw, uint2& tag) {
     const D4 a = W.ray_o[p], b = W.ray_d[p], t = W.thr[p];
-    r.o = v3(a.x, a.y, a.z); r.time = a.w;
+    r.o = v3(a.x, a.y, a.z); r.time = tw ? 0.0 : a.w;
     r.d = v3(b.x, b.y, b.z);
     r.key = 0;
     T = v3(t.x, t.y, t.z);
     unpack_u32x2(b.w, rng.x, rng.y);
     unpack_u32x2(t.w, rng.z, rng.w);
+    if (tw) unpack_u32x2(a.w, tag.x, tag.y);
+    else tag = W.tag[p];
 }
 __device__ __forceinline__ void store_path(const WfSet& W, uint32_t p, const Ray& r, const V3& T, const Rng& rng,
-                                           uint32_t item, uint32_t level = 0) {
+                                           uint32_t item, uint32_t level, bool tw) {
     D4 a, b, t;
-    a.x = r.o.x; a.y = r.o.y; a.z = r.o.z; a.w = r.time;
+    a.x = r.o.x; a.y = r.o.y; a.z = r.o.z; a.w = tw ? pack_u32x2(item, level) : r.time;
     b.x = r.d.x; b.y = r.d.y; b.z = r.d.z; b.w = pack_u32x2(rng.x, rng.y);
     t.x = T.x; t.y = T.y; t.z = T.z; t.w = pack_u32x2(rng.z, rng.w);
     W.ray_o[p] = a; W.ray_d[p] = b; W.thr[p] = t;
-    W.tag[p] = make_uint2(item, level);
+    if (!tw) W.tag[p] = make_uint2(item, level);
 }
 
 // Block-aggregated slot allocation for up to C independent counters: ONE returning atomic per
@@ -1410,13 +1419,13 @@ __global__ __launch_bounds__(kBlock) void k_wf_gen(DCamera C, PathParams P, WfSt
             h[0] = b - a;
             h[1] = a;
         }
-        if (live) store_path(W.set[0], i, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
+        if (live) store_path(W.set[0], i, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item, 0u, W.tagw);
         return;
     }
     publish_offsets(W, 0, n);
     const uint32_t sh = blockIdx.x % kShards;
     const uint32_t slot = block_slot1(live, shard_bank(W, 0) + sh * kShardStride);
-    if (live) store_path(W.set[0], shard_off(n, sh) + slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item);
+    if (live) store_path(W.set[0], shard_off(n, sh) + slot, r, v3(1.0, 1.0, 1.0), rng, (uint32_t)item, 0u, W.tagw);
 }
 #endif  // RS_TU_COMMON
 
@@ -1437,7 +1446,7 @@ __global__ __launch_bounds__(kBlock, SM == kSmFlat ? kWfExtFlatWaves : 1) void k
         const uint32_t v = base + threadIdx.x;
         if (v < n) {
             const uint32_t i = seg_pos(in, v);
-            Ray r = load_ray(cur, i);
+            Ray r = load_ray(cur, i, W.tagw);
             if (rich_of(SM) && S.has_media) r.key = load_rng(cur, i).medium_key();  // the segment's medium key
             double bend = RS_INF;
             int bp;
@@ -1523,7 +1532,7 @@ __global__ __launch_bounds__(kBlock, kWfExtFlatWaves) void k_wf_extend_dyn(const
                 else if (k - pn < pbn) j = pb + (k - pn);
                 if (j != UINT32_MAX) {
                     i = (int)j;
-                    r = load_ray(cur, j);
+                    r = load_ray(cur, j, W.tagw);
                     rq = make_rayf4(make_rayf(r.o, v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z)));
                     best = RS_INF; bend = RS_INF; best32 = __builtin_huge_valf();
                     bp = -1; node = S.root4; sp = 0; qh = 0; qt = 0;
@@ -1577,13 +1586,14 @@ __global__ __launch_bounds__(kBlock, LAMB ? RS_LAMB_WAVES : 1) void k_wf_shade(c
         uint32_t item = 0;
         if (v < n) {
             const uint32_t i = seg_pos(in, v);
-            load_path(cur, i, r, T, rng);
+            uint2 tg;
+            load_path(cur, i, r, T, rng, W.tagw, tg);
             if (rich_of(SM) && S.has_media) r.key = rng.medium_key();
             const double2 hb = W.hit[i];
             const int bp = (int)__double_as_longlong(hb.x);
             Hit h;
             const bool ok = finish_hit<SM>(S, bp, r, 0.0001, hb.y, h);
-            item = cur.tag[i].x;
+            item = tg.x;
             alive = shade_step<SM, LAMB ? RS_MAT_LAMBERTIAN : -1>(S, ok, h, r, T, L, rng);
             if (alive && bounce + 1 >= depth) {  // depth limit
                 L = close_path(L, T);
@@ -1593,7 +1603,7 @@ __global__ __launch_bounds__(kBlock, LAMB ? RS_LAMB_WAVES : 1) void k_wf_shade(c
         }
         const uint32_t sh = (base / kBlock) % kShards;
         const uint32_t slot = block_slot1(alive, out + sh * kShardStride);
-        if (alive) store_path(nxt, shard_off(n, sh) + slot, r, T, rng, item);
+        if (alive) store_path(nxt, shard_off(n, sh) + slot, r, T, rng, item, 0u, W.tagw);
     }
 }
 
@@ -1707,7 +1717,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                 live = camera_sample(C, P, g, r, rng);
                 if (!live) put_rad(rad, item, 0.0, 0.0, 0.0);
             } else {
-                r = load_ray(cur, i);
+                r = load_ray(cur, i, W.tagw);
                 live = true;
             }
         }
@@ -1761,7 +1771,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                     // registers it was traced from; a carried path's is in place. (Regenerating it in the
                     // shading instead measured 0.5 % slower on the bench frame and 5 % on C4: profiles/r5/ab.)
                     W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
-                    if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u);
+                    if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u, W.tagw);
                     done = false;
                 }
             }
@@ -1770,7 +1780,8 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                 if (gen) {
                     t4.x = t4.y = t4.z = 1.0;
                 } else {
-                    t4 = cur.thr[i]; item = cur.tag[i].x;
+                    t4 = cur.thr[i];
+                    item = W.tagw ? (uint32_t)(uint64_t)__double_as_longlong(cur.ray_o[i].w) : cur.tag[i].x;
                 }
                 put_rad(rad, item, 0.0 + t4.x * add.x, 0.0 + t4.y * add.y, 0.0 + t4.z * add.z);
             }
@@ -1822,8 +1833,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_wfs_finish(const DScene* __restri
         Ray r;
         V3 T;
         Rng rng;
-        load_path(cur, i, r, T, rng);
-        const uint2 tg = cur.tag[i];
+        uint2 tg;
+        load_path(cur, i, r, T, rng, W.tagw, tg);
         V3 L = v3(0.0, 0.0, 0.0);
         bool open = true;
         for (uint32_t lvl = tg.y; lvl < depth; ++lvl) {
@@ -1862,8 +1873,8 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     uint32_t item = 0, lvl = 0;
     if (j < n) {
         const uint32_t i = queue[j];
-        load_path(cur, i, r, T, rng);
-        const uint2 tg = cur.tag[i];
+        uint2 tg;
+        load_path(cur, i, r, T, rng, W.tagw, tg);
         item = tg.x;
         lvl = tg.y;
         const double2 hb = W.hit[i];
@@ -1908,7 +1919,7 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
     if (alive) {
         const uint32_t p = light_ray ? slot : W.cap - 1u - slot;
-        store_path(nxt, p, r, T, rng, item, lvl + 1u);
+        store_path(nxt, p, r, T, rng, item, lvl + 1u, W.tagw);
     }
 }
 
