@@ -1547,6 +1547,7 @@ FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D,
 struct Pending {
     Replica* R = nullptr;
     Slot* L = nullptr;
+    uint32_t rec_bytes = 104;       // a path record as the kernels write it (96: the tag in ray_o.w, tag_in_ray)
     hipStream_t stream = nullptr;   // the stream the frame ends on (the caller's, or the replica's own)
     bool empty = true;
     int kind = 0;                   // 0 megakernel, 1 bounce-synchronous wavefront, 2 streaming wavefront
@@ -1690,6 +1691,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     const uint32_t shade_blocks = (uint32_t)std::max(1, R.n_cu * std::max(1, R.shade_bpc));
     ensure_stack_overflow(s, R, (uint64_t)std::max(std::max(ext_blocks, shade_blocks), wide) * kBlock);
     const SceneRef ds = R.ref();
+    P.rec_bytes = tag_in_ray(ds) ? 96u : 104u;
     const int sm = s->scene_mode;
 
     auto new_ev = [&]() { hipEvent_t e; HIP_OK(hipEventCreate(&e)); return e; };
@@ -2045,7 +2047,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
                 const uint64_t dead_new = P.inj[l][t] - live_new;
                 const uint64_t ended = live - shaded;
                 seg += live;
-                kbytes += 64ull * old + 20ull * shaded + 104ull * live_new + 60ull * ended + 24ull * dead_new;
+                kbytes += 64ull * old + 20ull * shaded + (uint64_t)P.rec_bytes * live_new + 60ull * ended + 24ull * dead_new;
 #ifdef RS_DEV_KNOBS
                 if (s->dump_iters) {
                     const uint32_t* qn = q + kWfsStride;  // the next set's runs
