@@ -1935,6 +1935,8 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 // PS: the classes of this launch -- 0 all; 1 the lean ones (Lambertian, Metal, Dielectric: bounded to 4 waves);
 // 2 the heavy ones (DiffuseMetal's two ONBs and ReflectionPdf loop, the generic switch): rs_scene::shade_split
 template <int SM, bool G4, bool LOBJ, int PS>
+// (the nest-2 lean launch at 3 waves, no scratch: C4-shaped frame +0.4 %; at 5 waves +5.7 %:
+// profiles/r5/ab/n2_lean_waves_r6d.jsonl)
 #define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3)
 __global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
