@@ -564,7 +564,10 @@ __device__ __forceinline__ int bvh4_step(const DScene& S, const Ray& r, const Ra
 // whatever the order (equal t: the first met, as before), and the winner's record needs only a range
 // end above its own t.
 #define RS_LEAFQ 8      // entries per lane (power of two, >= 8)
-#define RS_LEAFQ_THR 48  // leaf pass at >= 48/64 of the working lanes with an entry queued
+#ifndef RS_LEAFQ_THR
+#define RS_LEAFQ_THR 48  // leaf pass at >= 48/64 of the working lanes with an entry queued (with the lane refill:
+                         // 32 / 40 / 56 -> +0.8 / -0.1 / +1.9 % of the mesh extend, profiles/r5/ab/c5_leafq_thr_r6h.jsonl)
+#endif
 template <int SM, class STK>
 __device__ __forceinline__ int bvh4_node_q(const DScene& S, const RayF4& rq, float tmin32, float best32, int node, int& sp,
                                            const STK& stk, int* q, int& qt) {
