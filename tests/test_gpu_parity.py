@@ -198,6 +198,35 @@ def test_pixel_mask_bounce_synchronous(gpu, name):
     assert np.array_equal(out, ref)
 
 
+def test_streaming_moving_sphere_records(gpu):
+    """A spheres-only scene with a moving sphere and a nonzero shutter runs the streaming wavefront with the
+    path's time in its record (WfState::tagw = 0: the (item, level) tag in its own array) and every sphere's
+    centre at the ray's time (sphere.rs center_at); the frame equals the oracle's. Its static twin (no speed)
+    carries the tag in ray_o.w and must differ only where the moving sphere is seen."""
+    from raysnail_amd.api import CameraBuilder, Color, Dielectric, DiffuseLight, Glass, Gradient, HittableList, \
+        Lambertian, Metal, Point3, Sphere, World
+    frames = []
+    for speed in ((0.6, 0.0, 0.2), None):
+        h, lights = HittableList(), HittableList()
+        h.add(Sphere((0.0, -1000.0, 0.0), 1000.0, Lambertian(Color(0.5, 0.5, 0.5, 1.0))))
+        s = Sphere((0.0, 1.0, 0.0), 1.0, Lambertian(Color(0.7, 0.3, 0.2, 1.0)))
+        h.add(s.with_speed(speed) if speed else s)
+        h.add(Sphere((2.2, 0.8, 0.5), 0.8, Metal(Color(0.7, 0.6, 0.5, 1.0))))
+        h.add(Sphere((-2.0, 0.7, 0.3), 0.7, Dielectric(Color(1.0, 1.0, 1.0, 1.0), 1.5).reflect_curve(Glass())))
+        light = Sphere((0.0, 6.0, 2.0), 1.0, DiffuseLight(Color(1.0, 0.9, 0.8, 1.0)).multiplier(4.0))
+        h.add(light)
+        lights.add(light)
+        cam = CameraBuilder().look_from(Point3(0.0, 2.0, 8.0)).look_at(Point3(0.0, 1.0, 0.0)).fov(35.0) \
+            .shutter_speed(1.0).width(64).height(40).build()
+        world = World(h, lights, Gradient(Color(0.3, 0.4, 0.5, 1.0), Color(0.7, 0.89, 1.0, 1.0)), (0.0, 1.0))
+        photo = cam.take_photo().samples(9).depth(12).seed(3)
+        img = photo.shot(None, world)
+        ref, _ = _oracle(world).render(cam.desc, photo.settings(), threads=8)
+        assert np.array_equal(img, ref)
+        frames.append(img)
+    assert not np.array_equal(frames[0], frames[1])
+
+
 def test_deep_paths_depth50(gpu):
     """Depth-50 recursion (configs 2-5): wavefront keeps bouncing until every queue drains."""
     for build in (lambda: scenes.rtow_13_1(40, 25)[:2], lambda: scenes.cornell_box(32, 32)):
