@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 LANES = int(os.environ.get("RS_LANES", "0"))  # wavefront lanes of the timed region (rs_scene_set_lanes; 0 = defaults)
-FRAMES = int(os.environ.get("RS_FRAMES", "0"))  # frames in flight (rs_scene_set_frames_in_flight; 0 = default 2)
+FRAMES = int(os.environ.get("RS_FRAMES", "0"))  # frames in flight (rs_scene_set_frames_in_flight; 0 = default 3)
 
 
 def log(*a):

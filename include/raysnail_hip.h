@@ -280,7 +280,7 @@ int rs_scene_get_info(const rs_scene* s, rs_scene_info* out);
  * counterpart (a scheduling knob like Painter::threads, painter.rs:318-325); frames are bitwise the
  * same. */
 int rs_scene_set_lanes(rs_scene* s, uint32_t lanes);
-/* frames in flight per device (1 .. 4; default 2): consecutive asynchronous frames are dealt to this
+/* frames in flight per device (1 .. 4; default 3): consecutive asynchronous frames are dealt to this
  * many frame slots, each with its own streams and buffers, and a frame waits only for the previous
  * frame of its slot -- the next frame's first paths are traced while the previous frame's last paths
  * drain. Output and stream semantics are unchanged: a frame's result is written on the call's stream,
@@ -290,7 +290,7 @@ int rs_scene_set_frames_in_flight(rs_scene* s, uint32_t frames);
 /* workspace sizes (0 = keep): camera samples per radiance batch buffer (default 32 Mi, whole sample
  * planes are used) and paths per path set (default 256 Mi: the bound of the streaming wavefront's pool
  * -- camera samples injected per iteration times the iterations a path can span; capped per device so
- * that the pools of its frame slots take at most half its memory -- and the chunk of the
+ * that the pools of its frame slots take at most two thirds of its memory -- and the chunk of the
  * bounce-synchronous wavefront). pool_paths is a soft bound: an iteration injects at least 256
  * samples (one block), so a pool below 256 x depth paths is raised to that for the frame.
  * Scheduling only: frames are bitwise the same for any value. */

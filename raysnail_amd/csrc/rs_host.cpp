@@ -279,7 +279,8 @@ struct rs_scene {
                                                   // the finish launch (k_wfs_finish; 0: none; never on nest-2 scenes)
     uint32_t wf_lanes = 2;                        // chunk lanes of the bounce-synchronous wavefront (rs_scene_set_lanes)
     uint32_t stream_lanes = 1;                    // lanes of the streaming wavefront (rs_scene_set_lanes)
-    uint32_t frames_in_flight = 2;                // frame slots per replica (rs_scene_set_frames_in_flight)
+    uint32_t frames_in_flight = 3;                // frame slots per replica (rs_scene_set_frames_in_flight; 3: bench frame
+                                                  // -0.6 %, its N = 8 row share -3 % against 2, profiles/r5/ab/frames_in_flight_r6*)
     bool ext_split = false;                       // streaming extend in two launches per iteration in every mode (dev A/B)
     bool shade_split = true;                      // spheres mode: lean / heavy material classes in two shading launches
     bool split_runs = false;                      // dev: carried front run / the rest in separate extend launches
@@ -1568,12 +1569,12 @@ struct Pending {
 };
 
 // The streaming pool of a frame on replica R: the scene's bound, capped so that the pools of all its frame slots
-// take at most half the device memory (a path's bytes, carve_wf: two sets of 3 x 32 B records + the tag, the hit,
-// a queue slot per class; 288 GB holds two slots of 256 Mi paths)
+// take at most two thirds of the device memory (a path's bytes, carve_wf: two sets of 3 x 32 B records + the tag,
+// the hit, a queue slot per class; 288 GB holds three slots of 256 Mi paths)
 uint32_t frame_slots(const rs_scene* s);
 uint64_t pool_limit(const rs_scene* s, const Replica& R) {
     const uint64_t per_path = 2 * (3 * sizeof(D4) + sizeof(uint2)) + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
-    return std::min<uint64_t>(s->pool_paths, std::max<uint64_t>(kBlock, R.mem_total / 2 / (frame_slots(s) * per_path)));
+    return std::min<uint64_t>(s->pool_paths, std::max<uint64_t>(kBlock, R.mem_total / 3 * 2 / (frame_slots(s) * per_path)));
 }
 
 // samples of a frame from which the spheres mode shades in two launches (rs_scene::shade_split)
