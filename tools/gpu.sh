@@ -161,6 +161,11 @@ for s in "$@"; do
       (cd $R && step 300 python3 tools/time_scene.py $v example 64 50 800x500 >> $OUT/c2.jsonl 2>> $OUT/c2.err) || { echo "c2 $v failed"; tail -5 $OUT/c2.err; exit 1; }
       echo "c2: $(tail -1 $OUT/c2.jsonl)"
     done ;;
+  benchprof)
+    # bench.py itself under rocprofv3 --kernel-trace --stats (the contract's "same command"): its bench line and the
+    # kernel statistics, whose k_wfs_extend average the line's event-timed avg_launch_ms should agree with
+    (cd /tmp && step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/benchprof -o bp -- python3 $R/bench.py --cpu-baseline 0 --row-share 0 > $OUT/bench_under_rocprof.json 2> $OUT/benchprof.err) || { echo "bench under rocprof failed"; tail -5 $OUT/benchprof.err; exit 1; }
+    tail -1 $OUT/bench_under_rocprof.json ;;
   meshtests)
     (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
     tail -1 $OUT/pytest_mesh.log ;;
