@@ -1578,7 +1578,10 @@ uint64_t pool_limit(const rs_scene* s, const Replica& R) {
 }
 
 // samples of a frame from which the spheres mode shades in two launches (rs_scene::shade_split)
-constexpr uint64_t kSplitShadeMin = 8ull << 20;
+#ifndef RS_SPLIT_SHADE_MIN  // (2 Mi, so the N = 8 row share's 3.2 M-sample frames split too: share 0.943 -> 0.968 ms
+#define RS_SPLIT_SHADE_MIN (8ull << 20)  // with three frame slots, profiles/r5/ab/split_shade_min_r6o.txt)
+#endif
+constexpr uint64_t kSplitShadeMin = RS_SPLIT_SHADE_MIN;
 
 // Frame slots a replica cycles through (render_enqueue takes slot next_slot % frame_slots): one for trees
 // whose traversal stack spills to the replica's shared HBM overflow array, else frames_in_flight. Callers
