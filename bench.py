@@ -74,6 +74,34 @@ def cpu_baseline(cam, world, spp, depth, seed, row_step, threads):
                       + (f" under a {quota}-CPU cgroup quota" if quota else "") + ", oracle/oracle.cpp f64"}
 
 
+def frame_model_bytes(segments, samples):
+    """SURVEY 8(d)'s frame-level algorithmic bytes: 212 B per path segment (extend: 28 B ray in,
+    16 B hit out; shade: 76 B state + 16 B hit in, 76 B state out) + 124 B per camera sample (generate: 76 B
+    state out; finalize: 16 B radiance + pixel in, 32 B float4 framebuffer read-modify-write)."""
+    return 212.0 * segments + 124.0 * samples
+
+
+def gather_rows_rank0_proxy(frame, world, bufs):
+    """Rank 0's share of distributed.gather_rows on one GPU: the pack copy of its rows, the arrival of all
+    `world` ranks' packed rows (a device copy of the same size stands in for the RCCL gather's writes into
+    rank 0's receive buffer), and the de-interleave into the full frame. Everything on the current stream,
+    like the real gather."""
+    import torch
+    H = frame.shape[0]
+    per = (H + world - 1) // world
+    if "packed" not in bufs:
+        bufs["packed"] = torch.zeros((per,) + tuple(frame.shape[1:]), dtype=frame.dtype, device=frame.device)
+        bufs["allp"] = torch.zeros((world, per) + tuple(frame.shape[1:]), dtype=frame.dtype, device=frame.device)
+        bufs["src"] = torch.zeros_like(bufs["allp"])
+        bufs["full"] = torch.empty((per * world,) + tuple(frame.shape[1:]), dtype=frame.dtype, device=frame.device)
+    packed, allp, src, full = bufs["packed"], bufs["allp"], bufs["src"], bufs["full"]
+    n = len(range(0, H, world))
+    packed[:n].copy_(frame[0::world])
+    allp.copy_(src)  # the gather's bytes landing in rank 0's receive buffer
+    full.view((per, world) + tuple(frame.shape[1:])).copy_(allp.transpose(0, 1))
+    return full[:H]
+
+
 def load_pmc(kernel_prefix):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary (tools/collect_pmc.py) and the
     profile round it was measured in (the field is only valid while the kernels are unchanged)."""
@@ -227,10 +255,31 @@ def main():
             sh_launch_ms += last["stats"].kernel_ms
         timed["on"] = False
         ds.set_lanes(LANES)
+        # the same share frames with rank 0's gather work after each (distributed.gather_rows: pack copy, the
+        # world's packed rows arriving -- a same-size device copy stands in for RCCL's writes --, de-interleave),
+        # pipelined like the real job's: the gather of frame f overlaps frame f+1's path kernels
+        gbufs = {}
+        for _ in range(args.warmup):
+            gather_rows_rank0_proxy(render(0, 0, K, 0), K, gbufs)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            gather_rows_rank0_proxy(render(0, 0, K, 0), K, gbufs)
+        torch.cuda.synchronize()
+        shg_ms = (time.perf_counter() - t1) / args.steps * 1e3
+        # the xGMI leg the proxy's device copy cannot show: each peer's packed rows over its own link into rank
+        # 0 (links in parallel), at the per-link figure the task states (7 links x ~153 GB/s per GPU)
+        per_rank_bytes = len(range(0, H, K)) * W * 16
+        xgmi_ms = per_rank_bytes / 153e9 * 1e3
         full_ms = dt / args.steps * 1e3
+        eff_g = full_ms / (K * (shg_ms + xgmi_ms))
         share = {"K": K, "rows": f"0::{K}", "ms_per_share": round(sh_ms, 4), "ms_full_frame": round(full_ms, 4),
-                 "predicted_efficiency": round(full_ms / (K * sh_ms), 4),
-                 "predicted_speedup": round(full_ms / sh_ms, 3),
+                 "predicted_efficiency_no_gather": round(full_ms / (K * sh_ms), 4),
+                 "ms_per_share_with_gather": round(shg_ms, 4), "gather_ms": round(shg_ms - sh_ms + xgmi_ms, 4),
+                 "gather_model": "rank-0 pack + same-size device copy + de-interleave, measured pipelined; plus "
+                                 f"{per_rank_bytes} B per peer over one xGMI link at 153 GB/s ({xgmi_ms:.4f} ms)",
+                 "predicted_efficiency": round(eff_g, 4),
+                 "predicted_speedup": round(K * eff_g, 3),
                  "extend_ms_per_share": round(sh_launch_ms / args.steps, 4),
                  "samples_per_share": int(last["stats"].samples), "launches_per_share": int(last["stats"].launches)}
 
@@ -255,6 +304,12 @@ def main():
                 "segments_per_launch": int(seg_per_launch), "launches_per_step": kern_launches // args.steps,
                 "kernel_share_of_step": round(kern_ms / args.steps / (dt / args.steps * 1e3), 4),
                 "segments_per_sample": round(segs / max(1, samples), 4)}
+        # the whole step against the same roofline: SURVEY 8(d)'s frame model over the pipelined step time
+        fbytes = frame_model_bytes(all_segs, all_samples) / max(1, args.steps)
+        roof["frame_model"] = "SURVEY 8(d): 212 B per segment + 124 B per sample, per step, over ms_per_step"
+        roof["frame_bytes_per_step"] = int(fbytes)
+        roof["achieved_frame"] = round(fbytes / (dt / args.steps) / 1e9, 2)
+        roof["frac_frame"] = round(roof["achieved_frame"] / HBM_PEAK_GBS, 5)
         # the library's own f64 byte model of the same launches (rs_render_stats.kernel_bytes: the
         # 32-byte path records, hits, queue slots and radiance this kernel actually moves), secondary
         if avg_launch_s > 0:

@@ -290,8 +290,10 @@ int rs_scene_set_frames_in_flight(rs_scene* s, uint32_t frames);
 /* workspace sizes (0 = keep): camera samples per radiance batch buffer (default 32 Mi, whole sample
  * planes are used) and paths per path set (default 256 Mi: the bound of the streaming wavefront's pool
  * -- camera samples injected per iteration times the iterations a path can span; capped per device so
- * that the pools of its frame slots take at most two thirds of its memory -- and the chunk of the
- * bounce-synchronous wavefront). pool_paths is a soft bound: an iteration injects at least 256
+ * that the pools of its frame slots and lanes take at most two thirds of its memory, and, when a frame
+ * slot allocates its pool, by the memory then free on the device (other allocations of the process
+ * shrink the pool instead of failing the render; RS_E_NOMEM only when not even a 256-path pool fits)
+ * -- and the chunk of the bounce-synchronous wavefront). pool_paths is a soft bound: an iteration injects at least 256
  * samples (one block), so a pool below 256 x depth paths is raised to that for the frame.
  * Scheduling only: frames are bitwise the same for any value. */
 int rs_scene_set_workspace(rs_scene* s, uint64_t max_batch_items, uint64_t pool_paths);

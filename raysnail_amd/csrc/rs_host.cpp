@@ -174,7 +174,7 @@ struct Slot {
     uint8_t* d_mask = nullptr; size_t mask_cap = 0;   // replicas > 0: the caller's mask copied over
     float* d_out = nullptr; size_t out_cap = 0;       // replicas > 0 / rs_render: the frame on this device
     // wavefront path state (capacity wf_cap paths per set) per lane + queue counters
-    void* d_wf = nullptr; size_t wf_cap = 0; uint32_t wf_lanes = 0;
+    void* d_wf = nullptr; size_t wf_cap = 0; uint32_t wf_lanes = 0; size_t wf_bytes = 0;
     uint32_t** d_qptrs[kMaxLanes] = {nullptr};    // per lane: device array of the per-class queues
     uint32_t* qptr[kMaxLanes][kWfsClasses] = {{nullptr}};
     WfState lane_ws[kMaxLanes]{};
@@ -272,7 +272,7 @@ struct rs_scene {
     // streaming pool bound (paths per set): a frame injects Q samples per iteration with Q * min(depth, iterations)
     // <= the pool, so a larger pool means fewer, fuller iterations on big depth-50 frames (C3 1920x1080x256:
     // 64 Mi 210.9 ms, 128 Mi 197.1 ms, 256 Mi 190.7 ms; profiles/r5/ab/pool_sizes_r5c.jsonl); each replica caps it
-    // by its device memory (Replica::pool_limit)
+    // by its device memory and, when a slot allocates, by what is free (pool_limit, pool_limit_free)
     uint64_t pool_paths = 256ull << 20;
     uint32_t inject_div = 1;                      // streaming: inject up to 1/inject_div of a lane per iteration
     uint32_t finish_after = 16;                   // streaming: wavefront iterations after the last injection before
@@ -283,7 +283,6 @@ struct rs_scene {
                                                   // -0.6 %, its N = 8 row share -3 % against 2, profiles/r5/ab/frames_in_flight_r6*)
     bool ext_split = false;                       // streaming extend in two launches per iteration in every mode (dev A/B)
     bool shade_split = true;                      // spheres mode: lean / heavy material classes in two shading launches
-    bool split_runs = false;                      // dev: carried front run / the rest in separate extend launches
     bool dump_iters = false;                      // dev: per-iteration queue counts to stderr (timed frames)
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
     int tree_depth = 0;                     // levels of the tree in use
@@ -1356,10 +1355,13 @@ uint32_t tag_in_ray(const SceneRef& s) {
 #endif
 }
 
+// bytes of one path of a wavefront pool (carve_wf): two sets of 3 x 32 B records + the tag, the hit, a slot per class queue
+constexpr uint64_t kPathBytes = 2 * (3 * sizeof(D4) + sizeof(uint2)) + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
+
 // Path state of `lanes` lanes of capacity `cap` paths per set each (L.lane_ws[l], L.d_qptrs[l], L.qptr[l]).
-void carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
-    const size_t per_set = 3 * sizeof(D4) + sizeof(uint2);
-    const size_t per = 2 * per_set + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
+// Returns false, with the slot holding no pool, when the device cannot allocate it (the caller shrinks the pool).
+bool carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
+    const size_t per = kPathBytes;
     const uint64_t c = (std::max<uint64_t>(cap, L.wf_cap) + 255) & ~(uint64_t)255;
     const size_t lane_bytes = (per * c + 16 * 256 + 8192 + 255) & ~(size_t)255;
     const bool fresh = c > L.wf_cap || lanes > L.wf_lanes;
@@ -1368,9 +1370,17 @@ void carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
         L.d_wf = nullptr;
         L.wf_cap = 0;
         L.wf_lanes = 0;
-        HIP_OK(hipMalloc(&L.d_wf, lane_bytes * lanes));
+        L.wf_bytes = 0;
+        const hipError_t e = hipMalloc(&L.d_wf, lane_bytes * lanes);
+        if (e == hipErrorOutOfMemory) {
+            (void)hipGetLastError();  // not sticky: clear it for the next call's checks
+            L.d_wf = nullptr;
+            return false;
+        }
+        HIP_OK(e);
         L.wf_cap = c;
         L.wf_lanes = lanes;
+        L.wf_bytes = lane_bytes * lanes;
     }
     auto al = [](char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); };
     for (uint32_t l = 0; l < lanes; ++l) {
@@ -1394,6 +1404,7 @@ void carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
         w.counts = nullptr;
         w.cap = (uint32_t)c;
     }
+    return true;
 }
 
 struct DeviceGuard {
@@ -1568,13 +1579,32 @@ struct Pending {
     }
 };
 
-// The streaming pool of a frame on replica R: the scene's bound, capped so that the pools of all its frame slots
-// take at most two thirds of the device memory (a path's bytes, carve_wf: two sets of 3 x 32 B records + the tag,
-// the hit, a queue slot per class; 288 GB holds three slots of 256 Mi paths)
+// The pool (paths per lane and set) of a frame on slot L of replica R streaming on `lanes` lanes: the scene's bound,
+// capped so that the pools of all the replica's frame slots take at most two thirds of the device memory (kPathBytes
+// per path and lane; 288 GB holds three slots of 256 Mi paths on one lane). A pool size is scheduling only: frames do
+// not depend on it (rs_host.cpp make_sched, tests/test_gpu_parity.py test_streaming_pool_and_async_bit_identical).
 uint32_t frame_slots(const rs_scene* s);
-uint64_t pool_limit(const rs_scene* s, const Replica& R) {
-    const uint64_t per_path = 2 * (3 * sizeof(D4) + sizeof(uint2)) + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
-    return std::min<uint64_t>(s->pool_paths, std::max<uint64_t>(kBlock, R.mem_total / 3 * 2 / (frame_slots(s) * per_path)));
+uint64_t pool_limit(const rs_scene* s, const Replica& R, uint32_t lanes) {
+    const uint64_t per = kPathBytes * std::max<uint32_t>(1, lanes);
+    return std::min<uint64_t>(s->pool_paths, std::max<uint64_t>(kBlock, R.mem_total / 3 * 2 / (frame_slots(s) * per)));
+}
+// ... and what the device can give it now: the memory free at render time (hipMemGetInfo) plus the pool this slot
+// already holds (freed before a larger one is allocated), shared with the replica's slots that have no pool yet,
+// less a tenth for the frame's other buffers. A caller that keeps other data on the device (a PyTorch caching
+// allocator, another scene) then gets a smaller pool instead of an allocation failure. Queried only when the slot
+// has to allocate.
+uint64_t pool_limit_free(const rs_scene* s, const Replica& R, const Slot& L, uint32_t lanes) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return kBlock;
+    }
+    const uint32_t n_slots = frame_slots(s);
+    uint32_t empty = 0;
+    for (uint32_t k = 0; k < n_slots; ++k)
+        if (&R.slots[k] == &L || !R.slots[k].d_wf) ++empty;
+    const uint64_t usable = ((uint64_t)free_b + (L.d_wf ? L.wf_bytes : 0)) / 10 * 9 / std::max<uint32_t>(1, empty);
+    return std::max<uint64_t>(kBlock, usable / (kPathBytes * std::max<uint32_t>(1, lanes)));
 }
 
 // samples of a frame from which the spheres mode shades in two launches (rs_scene::shade_split)
@@ -1610,10 +1640,9 @@ hipStream_t lane_stream(Slot& L, uint32_t l) {
 }
 
 // The camera samples lane ln injects at iteration t (InjParams).
-InjParams inj_params(const FrameSched& f, const LaneSched& ln, uint64_t t, uint64_t ring_items) {
+InjParams inj_params(const FrameSched& f, const LaneSched& ln, uint64_t t) {
     InjParams I{};
     I.n_new = ln.n_new(t);
-    I.ring = ring_items;
     if (I.n_new) {
         const uint64_t j0 = t * ln.Q, m = j0 / f.B;
         const uint32_t k = ln.batch[m];
@@ -1714,10 +1743,19 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         join_to_S();
         HIP_OK(launch_finalize(L.d_acc, d_out, fp, S));
     } else if (streaming) {
-        const FrameSched f = make_sched(s, n_pix, N, D, ext_spill ? 1u : std::min<uint32_t>(kMaxLanes, s->stream_lanes),
-                                        pool_limit(s, R));
+        const uint32_t want = ext_spill ? 1u : std::min<uint32_t>(kMaxLanes, s->stream_lanes);
+        uint64_t pool = pool_limit(s, R, want);
+        FrameSched f = make_sched(s, n_pix, N, D, want, pool);
+        if (f.cap > L.wf_cap || f.lanes > L.wf_lanes) {  // the slot allocates: as much as the device has free
+            const uint64_t fp = pool_limit_free(s, R, L, want);
+            if (fp < pool) { pool = fp; f = make_sched(s, n_pix, N, D, want, pool); }
+        }
+        while (!carve_wf(L, f.cap, f.lanes)) {  // the allocation still failed (memory taken meanwhile): halve
+            if (pool <= kBlock) throw Error(RS_E_NOMEM, "device memory exhausted: no room for a path pool");
+            pool = std::max<uint64_t>(kBlock, pool / 2);
+            f = make_sched(s, n_pix, N, D, want, pool);
+        }
         ensure(L, L.d_rad, L.rad_cap, (size_t)3 * f.ring * f.B);
-        carve_wf(L, f.cap, f.lanes);
         n_counts = f.n_counts;
         uint32_t* const prev_counts = L.d_counts;
         ensure(L, L.d_counts, L.counts_cap, n_counts);
@@ -1729,7 +1767,6 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         for (uint32_t l = 1; l < f.lanes; ++l) ls[l] = lane_stream(L, l);
         if (!L.acc_stream) HIP_OK(hipStreamCreateWithFlags(&L.acc_stream, hipStreamNonBlocking));
         if (!L.fork_ev) HIP_OK(hipEventCreateWithFlags(&L.fork_ev, hipEventDisableTiming));
-        const uint64_t ring_items = (uint64_t)f.ring * f.B;
         HIP_OK(hipEventRecord(L.fork_ev, L0));
         for (uint32_t l = 1; l < f.lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], L.fork_ev, 0));
         HIP_OK(hipStreamWaitEvent(L.acc_stream, L.fork_ev, 0));
@@ -1747,7 +1784,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         // samples: 1.013 -> 1.066 ms)
         const bool split_shade = s->shade_split && (uint64_t)n_pix * N >= kSplitShadeMin;
         size_t n_ext = 0;
-        for (const LaneSched& ln : f.lane) n_ext += ln.T * (split || s->split_runs ? 2 : 1);
+        for (const LaneSched& ln : f.lane) n_ext += ln.T * (split ? 2 : 1);
         P.kev.assign(timed ? 2 * n_ext : 0, nullptr);
         for (auto& e : P.kev) e = new_ev();
         P.ev.assign(timed ? 2 : 0, nullptr);  // path_ms: the frame's iterations
@@ -1769,7 +1806,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  uint32_t** qd = L.d_qptrs[l];
                  const uint32_t n_new = ln.n_new(t);
                  inj[l][t] = n_new;
-                 InjParams I = inj_params(f, ln, t, ring_items);
+                 InjParams I = inj_params(f, ln, t);
                  if (n_new) {
                      const uint64_t m = t * ln.Q / f.B;
                      // a batch taking over a ring buffer: after the batch `ring` earlier was accumulated
@@ -1780,7 +1817,12 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  }
                  if (ln.finish && t + 1 == ln.T) {  // the finish: every carried path to its end, one launch
                      const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + kBlock - 1) / kBlock);
+                     // timed with the extends: it traces the World::hit of every segment it runs (the statistics
+                     // count them on this iteration), so the dominant kernel's time covers the frame's segments
+                     if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki], cs));
                      HIP_OK(launch_wfs_finish(ds, WS, (uint32_t)t, D, L.d_rad, std::max<uint32_t>(1, b), sm, cs));
+                     if (timed) HIP_OK(hipEventRecord(P.kev[2 * ki + 1], cs));
+                     ++ki;
                      ++path_launches;
                      window[l] = 0;
                      while (m_done[l] < ln.batch.size() && ln.done_it(m_done[l]) == t)
@@ -1799,29 +1841,19 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  // that part alone: nest-0 example.sdl 8.95 -> 8.41 ms; the spheres mode's carried part runs at 5
                  // waves (ext_min_waves), bench frame 7.58 -> 7.31 ms (profiles/r5/ab; at 4 waves its parts had
                  // measured 2.8 % slower than the merged kernel, profiles/r4/ab/part_pick)
-                 const bool pick = true;
-#ifdef RS_DEV_KNOBS
-                 if (s->split_runs && n_new == 0 && !split && window[l]) {  // dev: the front run and the rest timed apart
-                     I.run = 1;
-                     extend(pick ? kExtCarried : kExtAll, window[l]);
-                     I.run = 2;
-                     extend(pick ? kExtCarried : kExtAll, window[l]);
-                     I.run = 0;
-                 } else
-#endif
                  if (split) {
                      extend(kExtCarried, window[l]);
                      extend(kExtCamera, n_new);
-                 } else if (pick && n_new == 0) {
+                 } else if (n_new == 0) {
                      extend(kExtCarried, window[l]);
-                 } else if (pick && window[l] == 0) {
+                 } else if (window[l] == 0) {
                      extend(kExtCamera, n_new);
                  } else {
                      extend(kExtAll, window[l] + n_new);
                  }
                  if (D > 0) {
                      const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + n_new + kBlock - 1) / kBlock);
-                     HIP_OK(launch_wfs_shade_all(ds, WS, qd, s->class_mask, (uint32_t)t, D, ring_items, L.d_rad, b,
+                     HIP_OK(launch_wfs_shade_all(ds, WS, qd, s->class_mask, (uint32_t)t, D, L.d_rad, b,
                                                  split_shade, sm, cs));
                      ++path_launches;
                  }
@@ -1839,7 +1871,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  const double* rk = L.d_rad + (size_t)3 * (k % f.ring) * f.B;  // item-major radiance (put_rad)
                  if (k + 1 < f.n_batches) {
                      HIP_OK(hipStreamWaitEvent(L.acc_stream, done_ev(k), 0));
-                     HIP_OK(launch_accumulate(rk, ring_items, L.d_acc, n_pix, planes, k == 0, 0, fp, d_out, nullptr, 0,
+                     HIP_OK(launch_accumulate(rk, L.d_acc, n_pix, planes, k == 0, 0, fp, d_out, nullptr, 0,
                                               L.acc_stream));
                      HIP_OK(hipEventRecord(acc_ev(k), L.acc_stream));
                  } else {
@@ -1853,7 +1885,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      HIP_OK(hipEventRecord(L.fork_ev, L0));
                      HIP_OK(hipStreamWaitEvent(S, L.fork_ev, 0));
                      const size_t nz = counted ? 0 : n_counts;
-                     HIP_OK(launch_accumulate(rk, ring_items, L.d_acc, n_pix, planes, k == 0, 1, fp, d_out, L.d_counts,
+                     HIP_OK(launch_accumulate(rk, L.d_acc, n_pix, planes, k == 0, 1, fp, d_out, L.d_counts,
                                               (uint32_t)nz, S));
                      L.counts_clean = nz;
                  }
@@ -1868,20 +1900,34 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         // other's work. Chunks are whole sample planes when the batch allows (camera-ray tile order,
         // gen_perm). Scenes whose traversal stack spills to HBM keep one lane (the overflow array is
         // shared by blockIdx).
-        uint32_t lanes = (wavefront && !ext_spill) ? std::min<uint32_t>(kMaxLanes, s->wf_lanes) : 1u;
-        uint64_t chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(pool_limit(s, R), (uint64_t)n_pix * spb));
-        if (lanes > 1) {
-            const uint64_t planes = (spb + lanes - 1) / lanes;
-            const uint64_t split = std::max<uint64_t>(kBlock, spb >= lanes ? (uint64_t)n_pix * planes
-                                                                           : ((uint64_t)n_pix * spb + lanes - 1) / lanes);
-            chunk = std::min(chunk, split);
-        }
-        uint64_t n_chunks_total = 0;
-        for (uint32_t s0 = 0; s0 < N; s0 += spb) n_chunks_total += ((uint64_t)n_pix * std::min(spb, N - s0) + chunk - 1) / chunk;
-        if (n_chunks_total < lanes) lanes = std::max<uint32_t>(1, (uint32_t)n_chunks_total);
+        const uint32_t want = (wavefront && !ext_spill) ? std::min<uint32_t>(kMaxLanes, s->wf_lanes) : 1u;
+        uint32_t lanes = want;
+        uint64_t chunk = 0, n_chunks_total = 0;
+        auto plan = [&](uint64_t pool) {  // chunks of at most `pool` paths per lane
+            lanes = want;
+            chunk = std::max<uint64_t>(kBlock, std::min<uint64_t>(pool, (uint64_t)n_pix * spb));
+            if (lanes > 1) {
+                const uint64_t planes = (spb + lanes - 1) / lanes;
+                const uint64_t split = std::max<uint64_t>(kBlock, spb >= lanes ? (uint64_t)n_pix * planes
+                                                                               : ((uint64_t)n_pix * spb + lanes - 1) / lanes);
+                chunk = std::min(chunk, split);
+            }
+            n_chunks_total = 0;
+            for (uint32_t s0 = 0; s0 < N; s0 += spb) n_chunks_total += ((uint64_t)n_pix * std::min(spb, N - s0) + chunk - 1) / chunk;
+            if (n_chunks_total < lanes) lanes = std::max<uint32_t>(1, (uint32_t)n_chunks_total);
+        };
+        uint64_t pool = pool_limit(s, R, want);
+        plan(pool);
         hipStream_t ls[kMaxLanes] = {L0};
         if (wavefront) {
-            carve_wf(L, chunk, lanes);
+            if (chunk > L.wf_cap || lanes > L.wf_lanes) {  // the slot allocates: as much as the device has free
+                const uint64_t fp = pool_limit_free(s, R, L, want);
+                if (fp < pool) plan(pool = fp);
+            }
+            while (!carve_wf(L, chunk, lanes)) {
+                if (pool <= kBlock) throw Error(RS_E_NOMEM, "device memory exhausted: no room for a path pool");
+                plan(pool = std::max<uint64_t>(kBlock, pool / 2));
+            }
             n_counts = (size_t)n_chunks_total * (D + 1);
             uint32_t* const prev_counts = L.d_counts;
             ensure(L, L.d_counts, L.counts_cap, n_counts);
@@ -1954,13 +2000,13 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
             if (timed) HIP_OK(hipEventRecord(P.ev[2 * bi + 1], L0));
             const bool last = s0 + spb >= N;
             if (!last) {
-                HIP_OK(launch_accumulate(L.d_rad, pp.n_items, L.d_acc, n_pix, nb, s0 == 0, 0, fp, d_out, nullptr, 0, L0));
+                HIP_OK(launch_accumulate(L.d_rad, L.d_acc, n_pix, nb, s0 == 0, 0, fp, d_out, nullptr, 0, L0));
             } else {
                 // the last batch's accumulate finishes the frame (into_color) and, when no statistics
                 // read the queue counters afterwards, zeroes them for the next frame (no memset launch)
                 join_to_S();
                 const size_t nz = (wavefront && !counted) ? n_counts : 0;
-                HIP_OK(launch_accumulate(L.d_rad, pp.n_items, L.d_acc, n_pix, nb, s0 == 0, 1, fp, d_out, L.d_counts,
+                HIP_OK(launch_accumulate(L.d_rad, L.d_acc, n_pix, nb, s0 == 0, 1, fp, d_out, L.d_counts,
                                          (uint32_t)nz, S));
                 L.counts_clean = nz;
             }
@@ -2361,7 +2407,6 @@ int rs_scene_create(rs_scene** out) {
         v = s->stream_lanes; knob("RS_SLANES", v); s->stream_lanes = (uint32_t)std::min<unsigned long long>(v, kMaxLanes);
         v = s->frames_in_flight; knob("RS_FRAMES", v); s->frames_in_flight = (uint32_t)std::min<unsigned long long>(v, kMaxSlots);
         v = 0; knob("RS_EXT_SPLIT", v); s->ext_split = v != 0;
-        v = 0; knob("RS_SPLIT_RUNS", v); s->split_runs = v != 0;
         v = 0; knob("RS_SHADE_MERGED", v); if (v) s->shade_split = false;
         v = 0; knob("RS_DUMP_ITERS", v); s->dump_iters = v != 0;
 #endif

@@ -118,9 +118,6 @@ struct InjParams {
     uint32_t nb1;         // items in the next batch (0: none)
     uint64_t g0, g1;      // frame items of the two batches' starts (k * batch: a lane's batches are not adjacent)
     uint32_t rad0, rad1;  // rad ring offsets of the two batches' buffers
-    uint64_t ring;        // rad channel stride (ring_batches * batch items)
-    uint32_t run;         // extend: 0 every record of the launch's part; 1 the carried front run only;
-                          // 2 the rest (dev builds time the two runs in separate launches)
 };
 
 struct FinalParams {
@@ -131,7 +128,7 @@ struct FinalParams {
 };
 
 // Megakernel: one thread per (pixel, sample) path (grid-stride over at most max_blocks blocks);
-// radiance -> rad[c * n_items + item].
+// radiance -> rad[3 * item + c] (item-major, rs_kernels.hip put_rad, like every path kernel).
 hipError_t launch_probe_sample(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, uint32_t x, uint32_t y,
                                uint32_t s0, uint32_t n, double* out, hipStream_t st);
 hipError_t launch_path_mega(const SceneRef& s, const DCamera& c, const PathParams& p, int sm, double* rad,
@@ -172,15 +169,14 @@ constexpr bool ext_split(int sm) { return sm == kSmNest2; }
 hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                              uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
                              int part, int sm, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present; ring: the
-// rad ring's items (batch buffers x batch items)
+// every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present
 // the streaming frame's last iteration: every carried path of set it&1 traced to its end, one thread each
 // (k_wfs_finish); blocks: at least one per 256 carried paths (grid-stride)
 hipError_t launch_wfs_finish(const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad, uint32_t blocks,
                              int sm, hipStream_t st);
 // split: the spheres mode's lean and heavy material classes in two launches (k_wfs_shade_all PS)
 hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
-                                uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, int sm,
+                                uint32_t it, uint32_t depth, double* rad, uint32_t blocks, bool split, int sm,
                                 hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids
 hipError_t wf_occupancy(int sm, int* extend_blocks_per_cu, int* shade_blocks_per_cu);
@@ -189,11 +185,11 @@ hipError_t launch_noise(const float* px, int w, int h, float t, uint8_t* redo, u
                         unsigned long long* count, hipStream_t st);
 hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, double tmin, double tmax, double* out,
                             hipStream_t st);
-// acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic; rad channel
-// stride `stride`); the last batch writes into_color of the sum into the frame instead (k_finalize's
+// acc[c * n_pix + pixel] += sum over the batch's samples in sample order (deterministic; item-major
+// radiance rad[3 * item + c], items sample-plane by sample-plane); the last batch writes into_color of the sum into the frame instead (k_finalize's
 // arithmetic, one launch less) and zeroes zero[0, n_zero) (the frame's queue counters) for the next
 // frame.
-hipError_t launch_accumulate(const double* rad, uint64_t stride, double* acc, uint32_t n_pix, uint32_t n_samp_batch,
+hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch,
                              int first_batch, int last_batch, const FinalParams& p, float* out_rgba, uint32_t* zero,
                              uint32_t n_zero, hipStream_t st);
 // into_color + RGBA f32 store into the full frame.

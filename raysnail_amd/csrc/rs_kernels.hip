@@ -1287,8 +1287,11 @@ __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_
     // A lattice with row step k (a strong-scaled share: rows r, r + k, ...) puts TH lattice rows
     // TH * k screen rows apart: keep the tile about square on screen (step 8: 64 x 1, step 2: 16 x 4)
     uint32_t TW = 8, TH = 8;
+#ifndef RS_SHARE_TH8
+#define RS_SHARE_TH8 1u  // lattice rows per tile at row step >= 8
+#endif
     if (P.row_step > 1) {
-        TH = P.row_step >= 8 ? 1u : P.row_step >= 4 ? 2u : 4u;
+        TH = P.row_step >= 8 ? RS_SHARE_TH8 : P.row_step >= 4 ? 2u : 4u;
         TW = 64u / TH;
     }
     const uint32_t npl = P.n_pix_local, W = P.width;
@@ -1698,11 +1701,8 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
     const uint32_t n = n_old + (PART == kExtCarried ? 0u : I.n_new);
     if (PART != kExtCamera && blockIdx.x == 0 && threadIdx.x == 0) cnt[0] = n_old;  // paths carried in (stats)
     const WfSet& cur = W.set[it & 1];
-    // the records of this launch: all, or (I.run, dev timing) the carried front run / the rest
-    const uint32_t j_lo = (PART != kExtCamera && I.run == 2) ? min(nf, n) : 0u;
-    const uint32_t j_hi = (PART != kExtCamera && I.run == 1) ? min(nf, n) : n;
-    const uint32_t base0 = j_lo + blockIdx.x * kBlock;
-    for (uint32_t base = base0; base < j_hi; base += gridDim.x * kBlock) {
+    const uint32_t base0 = blockIdx.x * kBlock;
+    for (uint32_t base = base0; base < n; base += gridDim.x * kBlock) {
         // thread -> record: the front run [0, nf), the back run from the set's end down, then the
         // injected camera samples, whose records follow the front run
         const uint32_t j = base + threadIdx.x;
@@ -1713,7 +1713,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
         Ray r;
         Rng rng;
         uint32_t item = 0;
-        if (j < j_hi) {
+        if (j < n) {
             if (gen) {
                 uint64_t g;
                 inj_sample(I, P, j - n_old, g, item);
@@ -1864,7 +1864,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_wfs_finish(const DScene* __restri
 template <int KIND, int SM>
 __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const uint32_t* __restrict__ queue,
                                                 uint32_t n, uint32_t base, uint32_t it, uint32_t* cnt_next, uint32_t depth,
-                                                uint64_t ring, double* __restrict__ rad) {
+                                                double* __restrict__ rad) {
     const WfSet& cur = W.set[it & 1];
     const WfSet& nxt = W.set[(it + 1) & 1];
     const uint32_t j = base + threadIdx.x;
@@ -1944,7 +1944,7 @@ template <int SM, bool G4, bool LOBJ, int PS>
 __global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    uint32_t* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
-                                                                                   uint32_t depth, uint64_t ring,
+                                                                                   uint32_t depth,
                                                                                    double* __restrict__ rad) {
     // (3 waves: 171 -> 168 VGPRs; at 4 waves it spilled 156 B, +6 %; nest-2 bounded at 3 spilled: C4 -21 %)
     DScene Sv;
@@ -1968,19 +1968,19 @@ __global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wf
         const uint32_t base = (v - first[k]) * kBlock;
         if (k == 0) {
             if constexpr ((kPart & 1u) != 0)
-                wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], n[0], base, it, cnt_next, depth, ring, rad);
+                wfs_shade_batch<RS_MAT_LAMBERTIAN, SM>(S, W, queues[0], n[0], base, it, cnt_next, depth, rad);
         } else if (k == 1) {
             if constexpr ((kPart & 2u) != 0)
-                wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], n[1], base, it, cnt_next, depth, ring, rad);
+                wfs_shade_batch<RS_MAT_METAL, SM>(S, W, queues[1], n[1], base, it, cnt_next, depth, rad);
         } else if (k == 2) {
             if constexpr ((kPart & 4u) != 0)
-                wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], n[2], base, it, cnt_next, depth, ring, rad);
+                wfs_shade_batch<RS_MAT_DIFFUSE_METAL, SM>(S, W, queues[2], n[2], base, it, cnt_next, depth, rad);
         } else if (k == 3 || !G4) {
             if constexpr ((kPart & 8u) != 0)
-                wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], n[3], base, it, cnt_next, depth, ring, rad);
+                wfs_shade_batch<RS_MAT_DIELECTRIC, SM>(S, W, queues[3], n[3], base, it, cnt_next, depth, rad);
         } else {
             if constexpr ((kPart & 16u) != 0)
-                wfs_shade_batch<-1, SM>(S, W, queues[NC - 1], n[NC - 1], base, it, cnt_next, depth, ring, rad);
+                wfs_shade_batch<-1, SM>(S, W, queues[NC - 1], n[NC - 1], base, it, cnt_next, depth, rad);
         }
     }
 }
@@ -1991,7 +1991,7 @@ __global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wf
 // channel), the batch's samples read 16 at a time (the adds stay in order): a strong-scaled share of
 // a frame has few pixels, and a thread per pixel looping over 3 x N dependent loads left the kernel
 // latency-bound (80 us for the N = 8 share of the bench frame).
-__global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict__ rad, uint64_t stride, double* __restrict__ acc,
+__global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict__ rad, double* __restrict__ acc,
                                                       uint32_t n_pix, uint32_t n_samp, int first, int last, FinalParams P,
                                                       float* __restrict__ out, uint32_t* __restrict__ zero, uint32_t n_zero) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -2004,7 +2004,6 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const double* __restrict_
     double a = first ? 0.0 : acc[(uint64_t)c * n_pix + p];
     const double* rc = rad + 3ull * p + c;
     const uint64_t sstep = 3ull * n_pix;
-    (void)stride;
     uint32_t s = 0;
     for (; s + 16 <= n_samp; s += 16) {
         double v[16];
@@ -2171,9 +2170,9 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
     X(hipError_t, wfs_finish, (const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad,        \
                                uint32_t blocks, hipStream_t st), (s, w, it, depth, rad, blocks, st))              \
     X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, \
-                                  uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, \
+                                  uint32_t it, uint32_t depth, double* rad, uint32_t blocks, bool split, \
                                   hipStream_t st),                                                              \
-      (s, w, queues, class_mask, it, depth, ring, rad, blocks, split, st))
+      (s, w, queues, class_mask, it, depth, rad, blocks, split, st))
 #define RS_DECLARE_SM(R, NAME, PARAMS, ARGS) template <int SMC> R NAME##_sm PARAMS;
 RS_SM_LAUNCHERS(RS_DECLARE_SM)
 RS_SORTED_LAUNCHERS(RS_DECLARE_SM)
@@ -2287,11 +2286,11 @@ hipError_t wfs_finish_sm(const SceneRef& s, const WfState& w, uint32_t it, uint3
 
 template <int SMC>
 hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, uint32_t it,
-                            uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, hipStream_t st) {
+                            uint32_t depth, double* rad, uint32_t blocks, bool split, hipStream_t st) {
     if (!blocks) return hipSuccess;
 #define RS_SHADE_LAUNCH(G4, LOBJ, PS, SHM)                                                                          \
     hipLaunchKernelGGL((k_wfs_shade_all<SMC, G4, LOBJ, PS>), dim3(blocks), dim3(kBlock), SHM, st, s.dev, w, queues, \
-                       class_mask, it, depth, ring, rad)
+                       class_mask, it, depth, rad)
     const uint32_t shm = s.host->limg_bytes;  // nest modes' LDS image (none in the spheres mode)
     if constexpr (SMC == kSmNest0 || SMC == kSmNest2) {
         // with the LDS image: the lean classes (leaf objects, classes 0-3 but DiffuseMetal) at 4 waves (128 VGPRs, 44 B
@@ -2385,9 +2384,9 @@ hipError_t launch_wfs_finish(const SceneRef& s, const WfState& w, uint32_t it, u
 }
 
 hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
-                                uint32_t it, uint32_t depth, uint64_t ring, double* rad, uint32_t blocks, bool split, int sm,
+                                uint32_t it, uint32_t depth, double* rad, uint32_t blocks, bool split, int sm,
                                 hipStream_t st) {
-    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, it, depth, ring, rad, blocks, split, st));
+    RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, it, depth, rad, blocks, split, st));
     return hipErrorInvalidValue;
 }
 
@@ -2417,12 +2416,12 @@ hipError_t launch_probe_hit(const SceneRef& s, const double* rays, uint32_t n, d
     return hipGetLastError();
 }
 
-hipError_t launch_accumulate(const double* rad, uint64_t stride, double* acc, uint32_t n_pix, uint32_t n_samp_batch,
+hipError_t launch_accumulate(const double* rad, double* acc, uint32_t n_pix, uint32_t n_samp_batch,
                              int first_batch, int last_batch, const FinalParams& p, float* out_rgba, uint32_t* zero,
                              uint32_t n_zero, hipStream_t st) {
     const uint32_t blocks = (uint32_t)((3ull * n_pix + kBlock - 1) / kBlock);
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kBlock), 0, st, rad, stride, acc, n_pix, n_samp_batch, first_batch,
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(kBlock), 0, st, rad, acc, n_pix, n_samp_batch, first_batch,
                        last_batch, p, out_rgba, zero, n_zero);
     return hipGetLastError();
 }

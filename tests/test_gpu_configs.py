@@ -79,3 +79,47 @@ def test_full_config_spp_rows_match_oracle(gpu, key, build, spp, k):
     ref, rs = _oracle(world).render(cam.desc, photo.rows(0, 0, k).settings(), threads=16)
     assert rs.samples == len(range(0, H, k)) * W * n
     _check(img, ref, slice(0, H, k))
+
+
+def test_pool_sized_from_free_memory(gpu):
+    """A C3-shaped frame (RTIOW 1920x1080, 256 spp, depth 50) rendered by a scene whose device is shared: a
+    torch tensor holds half the device (after the reference scene's own pool), so the three frame slots' full
+    256 Mi-path pools (~65 GB each) no longer fit. The pools are sized from the memory free when a slot
+    allocates (rs_host.cpp pool_limit_free): three asynchronous frames, one per slot, and a two-lane frame
+    equal the unconstrained frame bit for bit, or the call returns an RS_E_* code; it never aborts."""
+    import torch
+    from raysnail_amd import _abi as A
+    from raysnail_amd.api import RaysnailError
+    cam, world = scenes.rtow_13_1(1920, 1080)[:2]
+    st = cam.take_photo().samples(256).depth(50).seed(1).settings()
+    ref, rstats = world.device_scene().render(cam.desc, st)
+    free, total = torch.cuda.mem_get_info()
+    hold = torch.empty(max(0, min(total // 2, free - (8 << 30))), dtype=torch.uint8, device="cuda")
+    try:
+        cam2, world2 = scenes.rtow_13_1(1920, 1080)[:2]
+        ds = world2.device_scene()
+        outs = [torch.zeros((1080, 1920, 4), dtype=torch.float32, device="cuda") for _ in range(3)]
+        s = torch.cuda.current_stream().cuda_stream
+        ok = 0
+        try:
+            for o in outs:  # one frame per frame slot, back to back: each slot allocates its own pool
+                ds.render_device(cam2.desc, st, o.data_ptr(), s, stats=False)
+            torch.cuda.synchronize()
+            for o in outs:
+                assert np.array_equal(o.cpu().numpy(), ref)
+            ok += 1
+        except RaysnailError as e:
+            assert e.code in (A.RS_E_NOMEM, A.RS_E_HIP), e
+        del outs
+        ds.set_lanes(2)
+        try:
+            img, stats = ds.render(cam2.desc, st)
+            assert stats.segments == rstats.segments
+            assert np.array_equal(img, ref)
+            ok += 1
+        except RaysnailError as e:
+            assert e.code in (A.RS_E_NOMEM, A.RS_E_HIP), e
+        assert ok == 2, "the pools shrink to what is free: both renders are expected to succeed on a 288 GB device"
+    finally:
+        del hold
+        torch.cuda.empty_cache()

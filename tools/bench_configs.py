@@ -99,12 +99,29 @@ def main():
         tc = time.perf_counter() - t0
         cpu_msps = cst.samples / tc / 1e6
         same_rows = bool((img[::k] == ref[::k]).all())
+        # roofline (bench.py's fields): the dominant kernel's launches event-timed in the host-output frame above
+        # (its extends -- and the streaming finish, which traces the frame's last segments -- or the bounce-synchronous
+        # extends), SURVEY 8(d)'s 44 B per segment; and the frame model 212 B/segment + 124 B/sample over the
+        # device-resident frame time
+        from raysnail_amd._abi import KERNEL_NAMES
+        kl = max(1, st.kernel_launches)
+        alg = 44.0 * st.segments / kl
+        avg_s = st.kernel_ms / kl / 1e3
+        ach = alg / avg_s / 1e9 if avg_s > 0 else 0.0
+        fbytes = 212.0 * st.segments + 124.0 * st.samples
+        roof = {"bound": "hbm", "kernel": KERNEL_NAMES.get(st.kernel_id), "launches": st.kernel_launches,
+                "avg_launch_ms": round(avg_s * 1e3, 4), "alg_bytes_per_launch": int(alg),
+                "achieved": round(ach, 2), "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 5),
+                "kernel_share_of_frame": round(st.kernel_ms / (dt * 1e3), 4),
+                "frame_bytes": int(fbytes), "achieved_frame": round(fbytes / dt / 1e9, 2),
+                "frac_frame": round(fbytes / dt / 1e9 / 8000.0, 5)}
         out = {"config": key, "workload": desc, "width": W, "height": H, "spp": int(spp ** 0.5) ** 2,
                "depth": depth, "gpu": {"Msamples_per_s": round(gpu_msps, 2), "ms_per_frame": round(dt * 1e3, 2),
                                        "frames_timed": reps, "Gseg_per_s": round(st.segments / dt / 1e9, 3),
                                        "kernel_ms": round(st.kernel_ms, 2), "segments": st.segments,
                                        "segments_per_sample": round(st.segments / st.samples, 4),
                                        "launches": st.launches, "commit_s": round(t_commit, 3)},
+               "roofline": roof,
                "cpu_baseline": {"Msamples_per_s": round(cpu_msps, 4), "threads": args.cpu_threads, "kind": "port",
                                 "sample": f"rows 0::{k} ({cst.samples} samples) in {tc:.1f} s"},
                "speedup": round(gpu_msps / cpu_msps, 1), "sampled_rows_bit_identical": same_rows}

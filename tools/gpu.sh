@@ -17,7 +17,7 @@
 #   variants bench.py of base/, the product and every raysnail_amd/lib/var_*.so (tools/build_variant.sh), 2 rounds
 #   travstats per-category traversal counters (raysnail_amd/lib/trav_stats.so, a -DRS_TRAV_STATS build)
 #   abtrace  kernel traces of the bench frames, base/ then this tree (tools/trace_cmp.py)
-#   iters    per-iteration queue counts + per-run extend launches of the bench frame (dev library; tools/iter_table.py)
+#   iters    per-iteration queue counts + extend / shading launches of the bench frame (dev library; tools/iter_table.py)
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=$1; shift
@@ -165,7 +165,9 @@ for s in "$@"; do
     # bench.py itself under rocprofv3 --kernel-trace --stats (the contract's "same command"): its bench line and the
     # kernel statistics, whose k_wfs_extend average the line's event-timed avg_launch_ms should agree with
     (cd /tmp && step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/benchprof -o bp -- python3 $R/bench.py --cpu-baseline 0 --row-share 0 > $OUT/bench_under_rocprof.json 2> $OUT/benchprof.err) || { echo "bench under rocprof failed"; tail -5 $OUT/benchprof.err; exit 1; }
-    tail -1 $OUT/bench_under_rocprof.json ;;
+    tail -1 $OUT/bench_under_rocprof.json
+    # the line's roofline recomputed from the trace's statistics-frame launches (tools/trace_roofline.py)
+    (cd $R && python3 tools/trace_roofline.py $OUT/benchprof/bp_kernel_trace.csv $OUT/bench_under_rocprof.json | tee $OUT/trace_roofline.json) ;;
   meshtests)
     (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "mesh or c5 or C5 or million" > $OUT/pytest_mesh.log 2>&1) || { echo "mesh tests failed"; tail -30 $OUT/pytest_mesh.log; exit 1; }
     tail -1 $OUT/pytest_mesh.log ;;
@@ -184,13 +186,13 @@ for s in "$@"; do
     (cd /tmp && step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/abt_new -o t -- python3 $R/tools/render_once.py 0 5 > $OUT/abt_new.log 2>&1) || { echo "trace failed"; exit 1; }
     (cd $R && python3 tools/trace_cmp.py $OUT/abt_base/t_kernel_trace.csv $OUT/abt_new/t_kernel_trace.csv | tee $OUT/abtrace.txt) ;;
   iters)
-    # one lane, the dev library: per-iteration queue counts (RS_DUMP_ITERS) and the carried front run / the
-    # rest in separate extend launches (RS_SPLIT_RUNS) under a kernel trace; then the per-launch table
+    # one lane, the dev library: per-iteration queue counts (RS_DUMP_ITERS) under a kernel trace; then the
+    # per-iteration table (extend and shading launch times)
     # ITERSCENES="name spp depth;...": the frames (default the bench frame and C2's example.sdl frame)
     IFS=';' read -ra ISC <<< "${ITERSCENES:-rtow 64 8;example_sdl 64 50}"
     for sc in "${ISC[@]}"; do
       set -- $sc
-      (cd /tmp && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_DUMP_ITERS=1 RS_SPLIT_RUNS=1 step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/iters_$1 -o it -- python3 $R/tools/render_once.py 0 4 $1 $2 $3 > $OUT/iters_$1.log 2>&1) || { echo "iters trace $1 failed"; tail -5 $OUT/iters_$1.log; exit 1; }
+      (cd /tmp && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_DUMP_ITERS=1 step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/iters_$1 -o it -- python3 $R/tools/render_once.py 0 4 $1 $2 $3 > $OUT/iters_$1.log 2>&1) || { echo "iters trace $1 failed"; tail -5 $OUT/iters_$1.log; exit 1; }
       (cd $R && python3 tools/iter_table.py $OUT/iters_$1.log $(ls $OUT/iters_$1/*kernel_trace.csv) | tee $OUT/iters_$1.txt)
     done ;;
   configs)

@@ -1,7 +1,7 @@
-# dev: per-iteration table of the bench frame from a one-lane dev run with RS_DUMP_ITERS=1 RS_SPLIT_RUNS=1
-# (tools/gpu.sh iters): the queue counts the library printed per iteration and the kernel trace's launch
-# durations (extend of the carried front run = light-sample rays, extend of the rest = BSDF / other rays,
-# shading), averaged over the frames after the first; ns per path for each.
+# dev: per-iteration table of the bench frame from a one-lane dev run with RS_DUMP_ITERS=1 (tools/gpu.sh iters):
+# the queue counts the library printed per iteration and the kernel trace's launch durations (the extend --
+# 'ext rest' = all its records: the front-run / rest split of earlier rounds' dev builds is gone -- and the
+# shading), averaged over the frames after the first; ps per path for each.
 # usage: python tools/iter_table.py <iters.log> <kernel_trace.csv>
 import csv, re, sys
 from collections import defaultdict

@@ -25,9 +25,9 @@ for name in names:
     cam, world = build()
     photo = cam.take_photo().samples(spp).depth(depth).seed(1)
     photo.shot(None, world)
-    fn(out, 1)
+    assert fn(out, 1) == 0, "reading the counters failed (a fault in the frame before?)"
     photo.shot(None, world)
-    fn(out, 1)
+    assert fn(out, 1) == 0, "reading the counters failed (a fault in the frame before?)"
     for c, cname in enumerate(CATS):
         v = out[32 * c:32 * c + 32]
         nodes, leaves, rays, wmax, lanes, waves, witer = v[:7]
@@ -36,7 +36,10 @@ for name in names:
         print(f"{name} {cname:13s}: rays {rays} nodes/ray {nodes/max(rays,1):.2f} leaves/ray {leaves/max(rays,1):.2f} "
               f"wave-max nodes {wmax/max(waves,1):.2f} live lanes/wave {lanes/max(waves,1):.1f} "
               f"lane efficiency {(nodes/max(rays,1))/max(wmax/max(waves,1),1e-9):.3f} "
-              f"leaf passes/wave {witer/max(waves,1):.2f} leaf-pass lane use {leaves/max(64*witer,1):.3f}", flush=True)
+              # leaf passes exist only in the near-first walks (bvh4_step, the flat leaf FIFO); the nest modes'
+              # deferred walk lists a ray's leaves and tests them in a loop of its own (no passes counted)
+              + (f"leaf passes/wave {witer/max(waves,1):.2f} leaf-pass lane use {leaves/(64*witer):.3f}" if witer
+                 else "leaf passes n/a (deferred leaf list)"), flush=True)
         hist = list(v[8:24])
         tot = max(1, sum(hist))
         print("   node steps per ray, 8-wide buckets (%):", " ".join(f"{8*b}:{100*h/tot:.1f}" for b, h in enumerate(hist)),
