@@ -1334,6 +1334,23 @@ void ensure(Q& owner, T*& p, size_t& cap, size_t n) {
     HIP_OK(hipMalloc((void**)&p, n * sizeof(T)));
     cap = n;
 }
+// ensure() that reports an out-of-memory device as false (nothing held then) instead of throwing
+template <typename T, class Q>
+bool try_ensure(Q& owner, T*& p, size_t& cap, size_t n) {
+    if (n <= cap) return true;
+    if (p) { owner.quiesce(); HIP_OK(hipFree(p)); }
+    p = nullptr;
+    cap = 0;
+    const hipError_t e = hipMalloc((void**)&p, n * sizeof(T));
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        p = nullptr;
+        return false;
+    }
+    HIP_OK(e);
+    cap = n;
+    return true;
+}
 
 // Traversal-stack overflow for launches of at most `threads` grid threads: (stack_need - kStackMax)
 // entries per thread (DScene::stk_ovf). Nothing is allocated when the tree fits the LDS stack.
@@ -1588,12 +1605,12 @@ uint64_t pool_limit(const rs_scene* s, const Replica& R, uint32_t lanes) {
     const uint64_t per = kPathBytes * std::max<uint32_t>(1, lanes);
     return std::min<uint64_t>(s->pool_paths, std::max<uint64_t>(kBlock, R.mem_total / 3 * 2 / (frame_slots(s) * per)));
 }
-// ... and what the device can give it now: the memory free at render time (hipMemGetInfo) plus the pool this slot
-// already holds (freed before a larger one is allocated), shared with the replica's slots that have no pool yet,
-// less a tenth for the frame's other buffers. A caller that keeps other data on the device (a PyTorch caching
-// allocator, another scene) then gets a smaller pool instead of an allocation failure. Queried only when the slot
-// has to allocate.
-uint64_t pool_limit_free(const rs_scene* s, const Replica& R, const Slot& L, uint32_t lanes) {
+// ... and what the device can give it now: the memory free at render time (hipMemGetInfo) plus the pool and radiance
+// ring this slot already holds (freed before larger ones are allocated), shared with the replica's slots that have
+// no pool yet, each keeping `other` bytes (the frame's radiance ring) and 1 GiB (accumulation, counters, kernel
+// scratch) outside the pool. A caller that keeps other data on the device (a PyTorch caching allocator, another
+// scene) then gets a smaller pool instead of an allocation failure. Queried only when the slot has to allocate.
+uint64_t pool_limit_free(const rs_scene* s, const Replica& R, const Slot& L, uint32_t lanes, uint64_t other) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
         (void)hipGetLastError();
@@ -1603,8 +1620,19 @@ uint64_t pool_limit_free(const rs_scene* s, const Replica& R, const Slot& L, uin
     uint32_t empty = 0;
     for (uint32_t k = 0; k < n_slots; ++k)
         if (&R.slots[k] == &L || !R.slots[k].d_wf) ++empty;
-    const uint64_t usable = ((uint64_t)free_b + (L.d_wf ? L.wf_bytes : 0)) / 10 * 9 / std::max<uint32_t>(1, empty);
-    return std::max<uint64_t>(kBlock, usable / (kPathBytes * std::max<uint32_t>(1, lanes)));
+    const uint64_t mine = (L.d_wf ? L.wf_bytes : 0) + L.rad_cap * sizeof(double);
+    const uint64_t share = ((uint64_t)free_b + mine) / 10 * 9 / std::max<uint32_t>(1, empty);
+    const uint64_t keep = other + (1ull << 30);
+    return std::max<uint64_t>(kBlock, (share > keep ? share - keep : 0) / (kPathBytes * std::max<uint32_t>(1, lanes)));
+}
+// give back a slot's path pool and radiance ring (before a smaller pool is tried)
+void release_pool(Slot& L) {
+    if (!L.d_wf && !L.d_rad) return;
+    L.quiesce();
+    if (L.d_wf) HIP_OK(hipFree(L.d_wf));
+    if (L.d_rad) HIP_OK(hipFree(L.d_rad));
+    L.d_wf = nullptr; L.wf_cap = 0; L.wf_lanes = 0; L.wf_bytes = 0;
+    L.d_rad = nullptr; L.rad_cap = 0;
 }
 
 // samples of a frame from which the spheres mode shades in two launches (rs_scene::shade_split)
@@ -1746,16 +1774,22 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         const uint32_t want = ext_spill ? 1u : std::min<uint32_t>(kMaxLanes, s->stream_lanes);
         uint64_t pool = pool_limit(s, R, want);
         FrameSched f = make_sched(s, n_pix, N, D, want, pool);
-        if (f.cap > L.wf_cap || f.lanes > L.wf_lanes) {  // the slot allocates: as much as the device has free
-            const uint64_t fp = pool_limit_free(s, R, L, want);
+        auto rad_n = [&]() { return (size_t)3 * f.ring * f.B; };
+        // the smallest pool a frame is scheduled on: 64 Ki camera samples per iteration (or the whole frame); below
+        // that the iterations (and their counter blocks) multiply, and the render reports the device as full
+        const uint64_t pool_min = std::min<uint64_t>(f.cap, (uint64_t)65536 * std::max<uint32_t>(D, 1));
+        if (f.cap > L.wf_cap || f.lanes > L.wf_lanes || rad_n() > L.rad_cap) {
+            // the slot allocates: as much as the device has free
+            const uint64_t fp = std::max(pool_min, pool_limit_free(s, R, L, want, rad_n() * sizeof(double)));
             if (fp < pool) { pool = fp; f = make_sched(s, n_pix, N, D, want, pool); }
         }
-        while (!carve_wf(L, f.cap, f.lanes)) {  // the allocation still failed (memory taken meanwhile): halve
-            if (pool <= kBlock) throw Error(RS_E_NOMEM, "device memory exhausted: no room for a path pool");
-            pool = std::max<uint64_t>(kBlock, pool / 2);
+        // an allocation that still fails (memory taken meanwhile): both buffers back, half the pool
+        while (!carve_wf(L, f.cap, f.lanes) || !try_ensure(L, L.d_rad, L.rad_cap, rad_n())) {
+            release_pool(L);
+            if (pool <= pool_min) throw Error(RS_E_NOMEM, "device memory exhausted: no room for the frame's path pool");
+            pool = std::max<uint64_t>(pool_min, pool / 2);
             f = make_sched(s, n_pix, N, D, want, pool);
         }
-        ensure(L, L.d_rad, L.rad_cap, (size_t)3 * f.ring * f.B);
         n_counts = f.n_counts;
         uint32_t* const prev_counts = L.d_counts;
         ensure(L, L.d_counts, L.counts_cap, n_counts);
@@ -1920,13 +1954,14 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         plan(pool);
         hipStream_t ls[kMaxLanes] = {L0};
         if (wavefront) {
+            const uint64_t pool_min = std::min<uint64_t>(chunk, 1ull << 20);  // chunks of at least 1 Mi paths
             if (chunk > L.wf_cap || lanes > L.wf_lanes) {  // the slot allocates: as much as the device has free
-                const uint64_t fp = pool_limit_free(s, R, L, want);
-                if (fp < pool) plan(pool = fp);
+                const uint64_t fp = std::max(pool_min, pool_limit_free(s, R, L, want, L.rad_cap * sizeof(double)));
+                if (fp < pool) plan(pool = fp);  // (the slot's radiance buffer, allocated above, stays)
             }
             while (!carve_wf(L, chunk, lanes)) {
-                if (pool <= kBlock) throw Error(RS_E_NOMEM, "device memory exhausted: no room for a path pool");
-                plan(pool = std::max<uint64_t>(kBlock, pool / 2));
+                if (pool <= pool_min) throw Error(RS_E_NOMEM, "device memory exhausted: no room for the frame's path pool");
+                plan(pool = std::max<uint64_t>(pool_min, pool / 2));
             }
             n_counts = (size_t)n_chunks_total * (D + 1);
             uint32_t* const prev_counts = L.d_counts;

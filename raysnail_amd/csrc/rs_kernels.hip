@@ -298,6 +298,15 @@ __device__ __forceinline__ LTri ld_ltri(const LTri* arr, int i) {
 __device__ __forceinline__ void test_sphere_leaf(const DScene& S, const DSphere& sp, int e, const Ray& r, const RayC& rc,
                                                  double tmin, double& best, double& bend, int& bp) {
     double t;
+#ifdef RS_LEAF_TWICE  // dev bound (tools/build_variant.sh): the quadratic done twice, the copy's inputs opaque
+    {
+        DSphere s2 = sp;
+        asm volatile("" : "+v"(s2.c[0]), "+v"(s2.c[1]), "+v"(s2.c[2]), "+v"(s2.r2));
+        double t2;
+        const bool h2 = sphere_t_trav(s2, r, rc.a, tmin, best, t2, S.moving != 0);
+        asm volatile("" ::"v"(t2), "v"((int)h2));
+    }
+#endif
     if (!sphere_t_trav(sp, r, rc.a, tmin, best, t, S.moving != 0)) return;
     double lo[3], hi[3];
     if (!S.moving || (sp.v[0] == 0.0 && sp.v[1] == 0.0 && sp.v[2] == 0.0)) {  // host: c -/+ r (sphere.rs:117-124)
