@@ -1294,10 +1294,10 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
 // not depend on it. A batch that is not whole planes keeps the identity order.
 __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_t n, const PathParams& P) {
     // A lattice with row step k (a strong-scaled share: rows r, r + k, ...) puts TH lattice rows
-    // TH * k screen rows apart: keep the tile about square on screen (step 8: 64 x 1, step 2: 16 x 4)
+    // TH * k screen rows apart: keep the tile near square on screen (step >= 8: 16 x 4, 4-7: 32 x 2, 2-3: 16 x 4)
     uint32_t TW = 8, TH = 8;
 #ifndef RS_SHARE_TH8
-#define RS_SHARE_TH8 1u  // lattice rows per tile at row step >= 8
+#define RS_SHARE_TH8 4u  // lattice rows per tile at row step >= 8 (16 x 4 lattice = 16 x 25 screen px at step 8; 64 x 1: N = 8 share 0.9416 -> 0.9313 ms, 32 x 2: 0.9342; profiles/r6/ab/variants_r6c_leaf2_th.txt)
 #endif
     if (P.row_step > 1) {
         TH = P.row_step >= 8 ? RS_SHARE_TH8 : P.row_step >= 4 ? 2u : 4u;
