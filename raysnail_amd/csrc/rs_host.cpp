@@ -175,8 +175,8 @@ struct Slot {
     float* d_out = nullptr; size_t out_cap = 0;       // replicas > 0 / rs_render: the frame on this device
     // wavefront path state (capacity wf_cap paths per set) per lane + queue counters
     void* d_wf = nullptr; size_t wf_cap = 0; uint32_t wf_lanes = 0; size_t wf_bytes = 0;
-    uint32_t** d_qptrs[kMaxLanes] = {nullptr};    // per lane: device array of the per-class queues
-    uint32_t* qptr[kMaxLanes][kWfsClasses] = {{nullptr}};
+    QEnt** d_qptrs[kMaxLanes] = {nullptr};        // per lane: device array of the per-class queues
+    QEnt* qptr[kMaxLanes][kWfsClasses] = {{nullptr}};
     WfState lane_ws[kMaxLanes]{};
     uint32_t* d_counts = nullptr; size_t counts_cap = 0;
     size_t counts_clean = 0;  // leading entries of d_counts known to be zero (reset by the last frame's accumulate)
@@ -1372,8 +1372,9 @@ uint32_t tag_in_ray(const SceneRef& s) {
 #endif
 }
 
-// bytes of one path of a wavefront pool (carve_wf): two sets of 3 x 32 B records + the tag, the hit, a slot per class queue
-constexpr uint64_t kPathBytes = 2 * (3 * sizeof(D4) + sizeof(uint2)) + sizeof(double2) + kWfsClasses * sizeof(uint32_t);
+// bytes of one path of a wavefront pool (carve_wf): two sets of 3 x 32 B records + the tag, an entry per class queue
+// (the bounce-synchronous wavefront's hit array shares the queues' memory)
+constexpr uint64_t kPathBytes = 2 * (3 * sizeof(D4) + sizeof(uint2)) + kWfsClasses * sizeof(QEnt);
 
 // Path state of `lanes` lanes of capacity `cap` paths per set each (L.lane_ws[l], L.d_qptrs[l], L.qptr[l]).
 // Returns false, with the slot holding no pool, when the device cannot allocate it (the caller shrinks the pool).
@@ -1410,10 +1411,10 @@ bool carve_wf(Slot& L, uint64_t cap, uint32_t lanes) {
             t.thr = (D4*)p; p += sizeof(D4) * c;
             t.tag = (uint2*)p; p = al(p + sizeof(uint2) * c);
         }
-        w.hit = (double2*)p; p += sizeof(double2) * c;
-        uint32_t* qp[kWfsClasses];
-        for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (uint32_t*)p; p = al(p + sizeof(uint32_t) * c); }
-        L.d_qptrs[l] = (uint32_t**)p;
+        w.hit = (double2*)p;  // (bounce-synchronous wavefront; the streaming one's queues below)
+        QEnt* qp[kWfsClasses];
+        for (int k = 0; k < kWfsClasses; ++k) { qp[k] = (QEnt*)p; p = al(p + sizeof(QEnt) * c); }
+        L.d_qptrs[l] = (QEnt**)p;
         w.fetch = (uint32_t*)al(p + sizeof(qp));  // 1 KiB (kFetchCounters x kFetchStride words), zeroed by k_wf_gen
         w.heads = w.fetch + 256;                   // 2 KiB: 2 banks x 8 shards x 32 words
         if (fresh) HIP_OK(hipMemcpy(L.d_qptrs[l], qp, sizeof(qp), hipMemcpyHostToDevice));
@@ -1837,7 +1838,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                  WfState WS = L.lane_ws[l];
                  WS.tagw = tag_in_ray(ds);
                  WS.counts = L.d_counts + ln.cnt_off;
-                 uint32_t** qd = L.d_qptrs[l];
+                 QEnt** qd = L.d_qptrs[l];
                  const uint32_t n_new = ln.n_new(t);
                  inj[l][t] = n_new;
                  InjParams I = inj_params(f, ln, t);
@@ -2111,7 +2112,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         kbytes = 80ull * seg;
     } else {
         // the streaming extend's library byte model, per iteration: ray records in (64 B)
-        // per carried path; hit (16 B) + queue slot (4 B) per shaded segment; the record out (96 B + item
+        // per carried path; the queue entry with the hit (16 B) per shaded segment; the record out (96 B + item
         // + level) per live camera sample (written after its traversal for the ones that go on to shading:
         // an upper bound); radiance out (24 B) per path ending in extend, + its throughput record and item
         // in (36 B); radiance out for masked samples
@@ -2132,7 +2133,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
                 const uint64_t dead_new = P.inj[l][t] - live_new;
                 const uint64_t ended = live - shaded;
                 seg += live;
-                kbytes += 64ull * old + 20ull * shaded + (uint64_t)P.rec_bytes * live_new + 60ull * ended + 24ull * dead_new;
+                kbytes += 64ull * old + 16ull * shaded + (uint64_t)P.rec_bytes * live_new + 60ull * ended + 24ull * dead_new;
 #ifdef RS_DEV_KNOBS
                 if (s->dump_iters) {
                     const uint32_t* qn = q + kWfsStride;  // the next set's runs

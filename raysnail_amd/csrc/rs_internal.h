@@ -82,6 +82,15 @@ struct PathParams {
 
 // 32-byte path-state record (one wave load = 2 KiB contiguous)
 struct alignas(32) D4 { double x, y, z, w; };
+// A material-class queue entry of the streaming wavefront: the path's record slot in the current set and its
+// World::hit result (the winning prim; in the spheres mode the winner's t, otherwise the range end it was accepted
+// under), 16 bytes written by the extend in queue order, so the shading reads its batch's entries contiguously
+// instead of gathering the hit by record slot (a sparse class's 16-byte hit gather took a 128-byte line each)
+struct alignas(16) QEnt {
+    uint32_t i;
+    int32_t bp;
+    double t;
+};
 
 // Wavefront path state. 32-byte records per path per array, in two ping-pong sets: a launch reads
 // set t&1 and the survivors are written, compacted, into set (t+1)&1, so every kernel streams
@@ -98,7 +107,8 @@ struct WfSet {
 };
 struct WfState {
     WfSet set[2];
-    double2* hit;         // per slot of the current set: (prim as bits, accepted range end)
+    double2* hit;         // bounce-synchronous wavefront, per slot of the current set: (prim as bits, accepted range
+                          // end) -- the memory of the class queues, which only the streaming wavefront uses
     uint32_t* counts;     // counter block per launch step (stride kWfsStride / 1 words)
     uint32_t* fetch;      // k_wf_extend_dyn's chunk counters (flat scenes)
     uint32_t* heads;      // bounce-synchronous sets: 2 banks x 8 shards x (count, region offset) (rs_kernels.hip Segs)
@@ -167,7 +177,7 @@ constexpr int kExtAll = 0, kExtCarried = 1, kExtCamera = 2;
 // nest-2 scenes extend in two launches: the merged kernel needs 256 VGPRs + 2 AGPRs (one wave/SIMD)
 constexpr bool ext_split(int sm) { return sm == kSmNest2; }
 hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
-                             uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
+                             QEnt* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
                              int part, int sm, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // every material class of iteration `it` in one launch (k_wfs_shade_all); class_mask: classes present
 // the streaming frame's last iteration: every carried path of set it&1 traced to its end, one thread each
@@ -175,7 +185,7 @@ hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathPara
 hipError_t launch_wfs_finish(const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad, uint32_t blocks,
                              int sm, hipStream_t st);
 // split: the spheres mode's lean and heavy material classes in two launches (k_wfs_shade_all PS)
-hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
+hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, QEnt* const* queues, uint32_t class_mask,
                                 uint32_t it, uint32_t depth, double* rad, uint32_t blocks, bool split, int sm,
                                 hipStream_t st);
 // blocks per CU the extend / shade kernels can keep resident (occupancy API), for grid-stride grids

@@ -1694,7 +1694,7 @@ __device__ __forceinline__ void lds_scene(const DScene* __restrict__ Sp, DScene&
 // LOBJ: the scene's tables from its LDS image (lds_scene; the launch passes limg_bytes of dynamic LDS)
 template <int SM, bool OVF, int PART, bool LOBJ>
 __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_extend(const DScene* __restrict__ Sp, WfState W,
-                                                                          uint32_t* const* __restrict__ queues, uint32_t it,
+                                                                          QEnt* const* __restrict__ queues, uint32_t it,
                                                                           double* __restrict__ rad, DCamera C, PathParams P,
                                                                           InjParams I) {
     DScene Sv;
@@ -1717,7 +1717,8 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
         const uint32_t j = base + threadIdx.x;
         const bool gen = PART == kExtCamera || (PART == kExtAll && j >= n_old);
         const uint32_t i = gen ? nf + (j - n_old) : j < nf ? j : W.cap - 1u - (j - nf);
-        int cls = -1;
+        int cls = -1, qbp = 0;
+        double qt = 0.0;  // the queue entry's hit (cls >= 0)
         bool live = false;
         Ray r;
         Rng rng;
@@ -1746,7 +1747,7 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
             }
         if (live) {
             double bend = RS_INF;
-            // the spheres mode keeps the winner's t (W.hit: the shading's sphere_rec_at), the others the range end
+            // the spheres mode keeps the winner's t (the queue entry: the shading's sphere_rec_at), the others the range end
             constexpr bool kT = SM == kSmSpheres;
             const int bp = traverse<SM, StkT<OVF, stack_lds(SM)>, LOBJ, kT, kTop>(S, r, 0.0001, bend, stk);
             V3 add;
@@ -1782,7 +1783,8 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
                     // a camera sample that goes on to shading: its record (T = 1, level 0), written from the
                     // registers it was traced from; a carried path's is in place. (Regenerating it in the
                     // shading instead measured 0.5 % slower on the bench frame and 5 % on C4: profiles/r5/ab.)
-                    W.hit[i] = make_double2(__longlong_as_double((long long)bp), bend);
+                    qbp = bp;
+                    qt = bend;
                     if (gen) store_path(cur, i, r, v3(1.0, 1.0, 1.0), rng, item, 0u, W.tagw);
                     done = false;
                 }
@@ -1812,7 +1814,11 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
         uint32_t* const cs[kClasses] = {&cnt[cix(1)], &cnt[cix(2)], &cnt[cix(3)], &cnt[cix(4)], &cnt[cix(5)]};
         const uint32_t slot = block_slot<kClasses>(cls, cs, gen && live,
                                                    PART == kExtCarried ? nullptr : &cnt[cix(kCntStat0 + (int)(blockIdx.x % kStatLines))]);
-        if (cls >= 0) queues[cls][slot] = i;
+        if (cls >= 0) {
+            QEnt q;
+            q.i = i; q.bp = qbp; q.t = qt;
+            queues[cls][slot] = q;
+        }
     }
 }
 
@@ -1871,7 +1877,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_wfs_finish(const DScene* __restri
 // base .. base + 255 of a queue of n): finish the hit record, scatter, write the radiance of paths that
 // end and append the survivors to the next set. Must be called by every thread of the block (block_slot).
 template <int KIND, int SM>
-__device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const uint32_t* __restrict__ queue,
+__device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& W, const QEnt* __restrict__ queue,
                                                 uint32_t n, uint32_t base, uint32_t it, uint32_t* cnt_next, uint32_t depth,
                                                 double* __restrict__ rad) {
     const WfSet& cur = W.set[it & 1];
@@ -1884,19 +1890,19 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     Rng rng;
     uint32_t item = 0, lvl = 0;
     if (j < n) {
-        const uint32_t i = queue[j];
+        const QEnt q = queue[j];
+        const uint32_t i = q.i;
         uint2 tg;
         load_path(cur, i, r, T, rng, W.tagw, tg);
         item = tg.x;
         lvl = tg.y;
-        const double2 hb = W.hit[i];
-        const int bp = (int)__double_as_longlong(hb.x);
+        const int bp = q.bp;
         Hit h;
-        if constexpr (SM == kSmSpheres) {  // hb.y: the winner's t (k_wfs_extend kT)
+        if constexpr (SM == kSmSpheres) {  // q.t: the winner's t (k_wfs_extend kT)
             const DPrim P = S.prims[bp];
-            sphere_rec_at(S.spheres[P.idx], P.mat, r, hb.y, h);
+            sphere_rec_at(S.spheres[P.idx], P.mat, r, q.t, h);
         } else {
-            finish_hit<SM, (KIND >= 0)>(S, bp, r, 0.0001, hb.y, h);
+            finish_hit<SM, (KIND >= 0)>(S, bp, r, 0.0001, q.t, h);
         }
         const int mi = h.mat >= 0 ? h.mat : S.default_mat;
         const DMaterial& M0 = S.mats[mi];
@@ -1951,7 +1957,7 @@ template <int SM, bool G4, bool LOBJ, int PS>
 // profiles/r5/ab/n2_lean_waves_r6d.jsonl)
 #define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3)
 __global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
-                                                                                   uint32_t* const* __restrict__ queues,
+                                                                                   QEnt* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
                                                                                    uint32_t depth,
                                                                                    double* __restrict__ rad) {
@@ -2173,12 +2179,12 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
     X(hipError_t, wf_occupancy, (int* e, int* sh), (e, sh))
 #define RS_SORTED_LAUNCHERS(X)                                                                                 \
     X(hipError_t, wfs_extend, (const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,       \
-                               uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, \
+                               QEnt* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, \
                                int part, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1),                        \
       (s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1))                                                  \
     X(hipError_t, wfs_finish, (const SceneRef& s, const WfState& w, uint32_t it, uint32_t depth, double* rad,        \
                                uint32_t blocks, hipStream_t st), (s, w, it, depth, rad, blocks, st))              \
-    X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, \
+    X(hipError_t, wfs_shade_all, (const SceneRef& s, const WfState& w, QEnt* const* queues, uint32_t class_mask, \
                                   uint32_t it, uint32_t depth, double* rad, uint32_t blocks, bool split, \
                                   hipStream_t st),                                                              \
       (s, w, queues, class_mask, it, depth, rad, blocks, split, st))
@@ -2245,7 +2251,7 @@ hipError_t wf_occupancy_sm(int* e, int* sh) {
 [[maybe_unused]] static inline bool lds_only_stack(const SceneRef& s, int sm) { return s.host->stack_need + 3 <= stack_lds(sm); }
 
 template <int SMC>
-hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w, uint32_t* const* queues,
+hipError_t wfs_extend_sm(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w, QEnt* const* queues,
                          uint32_t it, const InjParams& inj, double* rad, uint32_t blocks, int part, hipStream_t st,
                          hipEvent_t ev0, hipEvent_t ev1) {
     if (!blocks) return hipSuccess;
@@ -2294,7 +2300,7 @@ hipError_t wfs_finish_sm(const SceneRef& s, const WfState& w, uint32_t it, uint3
 }
 
 template <int SMC>
-hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask, uint32_t it,
+hipError_t wfs_shade_all_sm(const SceneRef& s, const WfState& w, QEnt* const* queues, uint32_t class_mask, uint32_t it,
                             uint32_t depth, double* rad, uint32_t blocks, bool split, hipStream_t st) {
     if (!blocks) return hipSuccess;
 #define RS_SHADE_LAUNCH(G4, LOBJ, PS, SHM)                                                                          \
@@ -2380,7 +2386,7 @@ hipError_t wf_occupancy(int sm, int* e, int* sh) {
 }
 
 hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
-                             uint32_t* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
+                             QEnt* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
                              int part, int sm, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     RS_SM_SORTED_DISPATCH(sm, return wfs_extend_sm<SMC>(s, c, p, w, queues, it, inj, rad, blocks, part, st, ev0, ev1));
     return hipErrorInvalidValue;
@@ -2392,7 +2398,7 @@ hipError_t launch_wfs_finish(const SceneRef& s, const WfState& w, uint32_t it, u
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, uint32_t* const* queues, uint32_t class_mask,
+hipError_t launch_wfs_shade_all(const SceneRef& s, const WfState& w, QEnt* const* queues, uint32_t class_mask,
                                 uint32_t it, uint32_t depth, double* rad, uint32_t blocks, bool split, int sm,
                                 hipStream_t st) {
     RS_SM_SORTED_DISPATCH(sm, return wfs_shade_all_sm<SMC>(s, w, queues, class_mask, it, depth, rad, blocks, split, st));
