@@ -723,9 +723,11 @@ template <int L, int R> struct Obj {
         case PK_MEDIUM: {  // medium/constant.rs:42-84
             if (!R) return false;  // media exist only in the rich scene mode
             const DMedium M = S.media[P.idx];
-            Hit h1, h2;
-            if (!Obj<L - 1, R>::hit(S, M.boundary, r, -RS_INF, RS_INF, h1)) return false;
-            if (!Obj<L - 1, R>::hit(S, M.boundary, r, h1.t1 + 0.0001, RS_INF, h2)) return false;
+            // the boundary's two hits decide on their t1 alone: hit_t (the same t1 bit for bit, no record: a
+            // sphere boundary's (u, v) -- correctly rounded atan2 / asin in image-textured scenes -- is never read)
+            HitT h1, h2;
+            if (!Obj<L - 1, R>::hit_t(S, M.boundary, r, -RS_INF, RS_INF, h1)) return false;
+            if (!Obj<L - 1, R>::hit_t(S, M.boundary, r, h1.t1 + 0.0001, RS_INF, h2)) return false;
             double t1 = h1.t1, t2 = h2.t1;
             if (t1 < tmin) t1 = tmin;
             if (t2 > tmax) t2 = tmax;

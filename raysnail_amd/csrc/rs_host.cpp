@@ -1130,7 +1130,12 @@ void build(rs_scene* s) {
     }
     // reference-order scenes on the in-order 4-wide tree (collapse4_inorder), nest-0 / nest-2 modes (the
     // generic mode measured 3 % slower on it: X2)
-    if (s->ref_order && (s->scene_mode == kSmNest0 || s->scene_mode == kSmNest2) && root >= 0) {
+#ifndef RS_GENERIC_4W_MIN
+#define RS_GENERIC_4W_MIN 0xFFFFFFFFu
+#endif
+    const bool inorder4 = s->scene_mode == kSmNest0 || s->scene_mode == kSmNest2 ||
+                          (s->scene_mode == kSmGeneric && s->world.size() >= (size_t)RS_GENERIC_4W_MIN);
+    if (s->ref_order && inorder4 && root >= 0) {
         std::vector<HNode4> n4;
         int depth4 = 0;
         const int32_t r4 = collapse4_inorder(B.nodes, root, n4, 0, depth4);
