@@ -126,6 +126,12 @@ def main():
                                 "sample": f"rows 0::{k} ({cst.samples} samples) in {tc:.1f} s"},
                "speedup": round(gpu_msps / cpu_msps, 1), "sampled_rows_bit_identical": same_rows}
         print(json.dumps(out), flush=True)
+        # the next config's frame slots size their pools from the memory then free (rs_host.cpp pool_limit_free):
+        # give this config's scene back first (its world holds the device scene, the oracle scene its world)
+        del ds, world, orc, img, ref, frame, photo, cam
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
