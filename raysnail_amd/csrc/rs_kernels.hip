@@ -692,7 +692,7 @@ __device__ __forceinline__ int traverse_flat_q(const DScene& S, const Ray& r, do
 // interleaved walk would test, in order. The walk's and the tests' registers are never live together.
 // A ray with more leaves walks again
 // for the next kLeafBatch (the LDS-image scenes' trees are a few nodes). The host gives a scene its LDS
-// image only when stack_need + kLeafBatch <= kStackMax and the tree is the in-order 4-wide one.
+// image only when stack_need + kLeafBatch <= stack_lds(mode) and the tree is the in-order 4-wide one.
 template <int SM, class STK>
 __device__ __forceinline__ int traverse_deferred(const DScene& S, const Ray& r, double tmin, double& bend_out, const STK& stk) {
     constexpr uint32_t K = kLeafBatch;

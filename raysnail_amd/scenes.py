@@ -396,6 +396,32 @@ def mesh_scene(width: int = 1920, height: int = 1080, n_theta: int = 120, n_phi:
     return cam, World(h, lights, Gradient(C32(0.3, 0.4, 0.5), C32(0.7, 0.89, 1.0)), (0.0, 0.0))
 
 
+def deep_spheres(width: int = 800, height: int = 500, n: int = 40000, seed: int = 5):
+    """A synthetic spheres-only scene whose 4-wide tree is deep (not a reference scene: a stress case for the
+    spheres mode's traversal stack past its LDS part): n small Lambertian / Metal spheres scattered over a
+    60 x 60 field at random heights, the RTIOW ground, light and camera."""
+    g = np.random.default_rng(seed)
+    h = HittableList()
+    h.add(Sphere((0.0, -1000.0, 0.0), 1000.0, Lambertian(C32(0.5, 0.5, 0.5))))
+    xyz = g.uniform((-30.0, 0.0, -30.0), (30.0, 3.0, 30.0), size=(n, 3))
+    rad = g.uniform(0.03, 0.15, size=n)
+    kind = g.uniform(size=n)
+    col = g.uniform(0.1, 0.9, size=(n, 3))
+    for k in range(n):
+        c = tuple(float(v) for v in xyz[k])
+        if kind[k] < 0.85:
+            mat = Lambertian(C32(*col[k]))
+        else:
+            mat = Metal(C32(*col[k]))
+        h.add(Sphere(c, float(rad[k]), mat))
+    lights = HittableList()
+    light = Sphere((300.0, 400.0, 100.0), 12.0, DiffuseLight(C32(1.0, 0.9, 0.7)).multiplier(1.5))
+    lights.add(light)
+    h.add(light)
+    cam = balls_scene_camera().width(width).height(height).build()
+    return cam, World(h, lights, Gradient(C32(0.3, 0.4, 0.5), C32(0.7, 0.89, 1.0)), (0.0, cam.shutter_speed))
+
+
 def cornell_smoke(width: int = 600, height: int = 600):
     """cornell_box_scene(carton = true, carton_rotation = true, smoke = true) (scene.rs:211-334): the
     light x7 over the larger rect, the two rotated boxes as ConstantMedium(white / black, 0.01)."""

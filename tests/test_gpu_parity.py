@@ -553,3 +553,18 @@ def test_render_rows_stats_on_spilling_mesh(gpu):
     assert np.array_equal(img, ref)
     assert (bst.samples, bst.segments) == (rst.samples, rst.segments)
     assert bst.kernel_bytes == rst.kernel_bytes
+
+
+def test_deep_spheres_stack_spill_matches_oracle(gpu):
+    """A spheres-mode scene whose 4-wide tree needs a 22-entry traversal stack (40k spheres): the entries past
+    the LDS part spill to the HBM overflow array, the replica runs one frame slot, and the frame still equals
+    the oracle's bit for bit with the same world.hit count."""
+    cam, world = scenes.deep_spheres(48, 32, 40000)
+    ds = world.device_scene()
+    info = ds.info()
+    assert info.scene_mode == 1 and info.stack_need > info.stack_lds
+    st = cam.take_photo().samples(9).depth(8).seed(3).settings()
+    img, stats = ds.render(cam.desc, st)
+    ref, rs = _oracle(world).render(cam.desc, st)
+    assert stats.segments == rs.segments
+    assert np.array_equal(img, ref)

@@ -20,7 +20,8 @@ def mesh_inside():
     return cam, world
 build = {"mesh": lambda: scenes.mesh_scene(W, H), "rtow": lambda: scenes.rtow_13_1(W, H)[:2], "mesh_in": mesh_inside,
          "quadric": lambda: scenes.quadric_sdl(W, H), "example": lambda: scenes.example_sdl(W, H),
-         "all_feature": lambda: scenes.all_feature_scene(W, H), "smoke": lambda: scenes.cornell_smoke(W, H)}[name]
+         "all_feature": lambda: scenes.all_feature_scene(W, H), "smoke": lambda: scenes.cornell_smoke(W, H),
+         "deep": lambda: scenes.deep_spheres(W, H)}[name]
 cam, world = build()
 photo = cam.take_photo().samples(spp).depth(depth).seed(1)
 photo.shot(None, world)
