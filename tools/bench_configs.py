@@ -43,7 +43,20 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=len(os.sched_getaffinity(0)) + 1,
                     help="default num_cpus + 1 like Painter::draw (painter.rs:321-325)")
     ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--inproc", action="store_true", help="run the configs in this process (default: one process each)")
     args = ap.parse_args()
+    if not args.inproc:
+        # one process per config: a config's frame slots size their pools from the memory free when they allocate
+        # (rs_host.cpp pool_limit_free), so nothing of the previous config's scene may still be held
+        import subprocess
+        keys = [k for k in configs() if not args.only or k in set(filter(None, args.only.split(",")))]
+        for key in keys:
+            cmd = [sys.executable, os.path.abspath(__file__), "--inproc", "--only", key, "--cpu-seconds", str(args.cpu_seconds),
+                   "--cpu-threads", str(args.cpu_threads), "--mode", str(args.mode)]
+            r = subprocess.run(cmd)
+            if r.returncode != 0:
+                sys.exit(r.returncode)
+        return
     import torch
     torch.cuda.set_device(0)
     from oracle.binding import OracleScene
@@ -126,12 +139,6 @@ def main():
                                 "sample": f"rows 0::{k} ({cst.samples} samples) in {tc:.1f} s"},
                "speedup": round(gpu_msps / cpu_msps, 1), "sampled_rows_bit_identical": same_rows}
         print(json.dumps(out), flush=True)
-        # the next config's frame slots size their pools from the memory then free (rs_host.cpp pool_limit_free):
-        # give this config's scene back first (its world holds the device scene, the oracle scene its world)
-        del ds, world, orc, img, ref, frame, photo, cam
-        import gc
-        gc.collect()
-        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
