@@ -40,6 +40,7 @@
  *   rs_render                TakePhotoSettings::shot_to_target src/camera.rs:261-287 (CameraBuilder
  *                            src/camera.rs:300-413; Painter src/painter.rs:69-336)
  *   rs_render_device         same, with the frame left in device memory (no PCIe in the timed region)
+ *   rs_render_device_passes  the CLI pass loop's renders (no redo map)  src/bin/raysnail.rs:379-427, as one call
  *
  * Output layout is the reference's Vec<[f32;4]>: W*H RGBA float32, row-major, row 0 = top,
  * sqrt-gamma applied when gamma != 0, unclamped, alpha 1.0 for rendered pixels, [0,0,0,0] for
@@ -68,7 +69,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 5
+#define RS_ABI_VERSION 6
 
 /* ---- status codes ---- */
 #define RS_OK             0
@@ -327,6 +328,17 @@ int rs_render_rows(rs_scene* s, const rs_camera_desc* cam, const rs_render_setti
  * the devices (kernel_ms / path_ms are device time, ms is the call's wall time). */
 int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st,
                      const uint8_t* d_mask, float* d_out_rgba, void* stream, rs_render_stats* stats);
+/* n_passes progressive passes of one frame into device frames: pass st->pass + k into d_outs[k] (k < n_passes;
+ * the pointers may repeat: later passes overwrite), each frame bitwise the one rs_render_device renders for that
+ * pass (no mask: the CLI's pass loop with its never-applied redo map, src/bin/raysnail.rs:379-427). Streaming
+ * scene modes (spheres, box / CSG: rs_scene_info.scene_mode 1, 3, 4) on one device run the passes as one sample
+ * stream: pass k + 1's camera samples enter the path pool while pass k's paths drain, so the small late launches of
+ * a pass are filled with the next one's work (a frame's share of a strong-scaled multi-GPU render is a few million
+ * samples); other scenes and several devices render the passes one rs_render_device call after the other. Stream
+ * and stats semantics as rs_render_device (stats summed over the passes). No reference counterpart as one call:
+ * the reference renders its passes one after the other (raysnail.rs:379). */
+int rs_render_device_passes(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, uint32_t n_passes,
+                            float* const* d_outs_rgba, void* stream, rs_render_stats* stats);
 
 /* ---- progressive passes (the CLI's pass loop, src/bin/raysnail.rs:311-427) ----
  * Device-resident frames (RGBA f32, W*H*4), all work on the caller's stream (NULL = default). */

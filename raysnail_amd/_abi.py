@@ -139,7 +139,7 @@ SCENE_SIGNATURES = {
 ROW_CALLBACK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.POINTER(C.c_float), C.c_uint32)
 
 _LIB = None
-ABI_VERSION = 5  # include/raysnail_hip.h RS_ABI_VERSION
+ABI_VERSION = 6  # include/raysnail_hip.h RS_ABI_VERSION
 
 
 def lib_path() -> str:
@@ -184,6 +184,9 @@ def load() -> C.CDLL:
                               C.POINTER(rs_render_stats)]
     lib.rs_render_device.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), VP, VP, VP,
                                      C.POINTER(rs_render_stats)]
+    lib.rs_render_device_passes.argtypes = [VP, C.POINTER(rs_camera_desc), C.POINTER(rs_render_settings), C.c_uint32,
+                                            C.POINTER(VP), VP, C.POINTER(rs_render_stats)]
+    lib.rs_render_device_passes.restype = C.c_int
     lib.rs_probe_world_hit.argtypes = [VP, VP, C.c_uint32, C.c_double, C.c_double, VP]
     lib.rs_scene_get_info.argtypes = [VP, C.POINTER(rs_scene_info)]
     lib.rs_scene_commit_devices.argtypes = [VP, C.POINTER(C.c_int), C.c_int]
@@ -209,6 +212,6 @@ EXPORTED_SYMBOLS = [
     "rs_scene_destroy", "rs_perlin", "rs_image", "rs_material", "rs_sphere", "rs_aarect", "rs_box", "rs_quadric", "rs_triangles", "rs_intersection",
     "rs_difference", "rs_transformed", "rs_constant_medium", "rs_world_add", "rs_lights_add", "rs_set_background", "rs_set_time_range",
     "rs_scene_commit", "rs_scene_commit_devices", "rs_scene_get_info", "rs_scene_set_lanes",
-    "rs_scene_set_frames_in_flight", "rs_scene_set_workspace", "rs_render", "rs_render_rows", "rs_render_device", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
+    "rs_scene_set_frames_in_flight", "rs_scene_set_workspace", "rs_render", "rs_render_rows", "rs_render_device", "rs_render_device_passes", "rs_combine_pixels_device", "rs_noise_map_device", "rs_noise_map",
     "rs_probe_world_hit", "rs_probe_samples",
 ]

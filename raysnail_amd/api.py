@@ -613,6 +613,17 @@ class DeviceScene:
                                                    C.byref(out) if stats else None), "rs_")
         return out
 
+    def render_device_passes(self, cam: A.rs_camera_desc, st: A.rs_render_settings, d_out_ptrs, stream_ptr: int = 0,
+                             stats: bool = True):
+        """rs_render_device_passes: passes st.pass + k into the device frames d_out_ptrs[k] (one sample stream on
+        streaming scenes). stats as render_device."""
+        n = len(d_out_ptrs)
+        ptrs = (C.c_void_p * max(1, n))(*[C.c_void_p(p) for p in d_out_ptrs])
+        out = A.rs_render_stats() if stats else None
+        _check(self.lib, self.lib.rs_render_device_passes(self.handle, C.byref(cam), C.byref(st), n, ptrs,
+                                                          stream_ptr or None, C.byref(out) if stats else None), "rs_")
+        return out
+
 
 # ----------------------------------------------------------------------------- camera ----
 class Camera:

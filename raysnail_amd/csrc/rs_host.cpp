@@ -284,6 +284,7 @@ struct rs_scene {
     bool ext_split = false;                       // streaming extend in two launches per iteration in every mode (dev A/B)
     bool shade_split = true;                      // spheres mode: lean / heavy material classes in two shading launches
     bool dump_iters = false;                      // dev: per-iteration queue counts to stderr (timed frames)
+    uint32_t passes_stream = 0;                   // rs_render_device_passes: 0 where it pays, 1 always, 2 never (dev A/B)
     uint32_t class_mask = (1u << kWfsClasses) - 1;  // shading classes some prim has (empty queues are not launched)
     int tree_depth = 0;                     // levels of the tree in use
     int tree_arity = 0;                     // 4: 4-wide tree, 2: binary tree, 0: empty world
@@ -1482,6 +1483,8 @@ struct LaneSched {
 struct FrameSched {
     uint64_t B = 0;
     uint32_t n_batches = 0, lanes = 1, ring = 1;
+    uint32_t nbpf = 0;                  // batches per frame (a multi-pass stream: frame k / nbpf, its batch k % nbpf)
+    std::vector<uint64_t> keys;         // per frame: PathParams::key_base of its pass
     std::vector<LaneSched> lane;
     uint64_t n_counts = 0;              // counter words of all lanes
     uint64_t cap = 0;                   // pool records per set (the largest lane's)
@@ -1507,20 +1510,25 @@ void walk(const FrameSched& f, FI visit, FA acc) {
         }
     }
 }
-FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D, uint32_t want_lanes, uint64_t pool) {
+FrameSched make_sched(const rs_scene* s, uint64_t n_pix, uint32_t N, uint32_t D, uint32_t want_lanes, uint64_t pool,
+                      uint32_t n_frames = 1) {
     FrameSched f;
-    // batches: at most max_items_per_batch items, and at least one per lane
+    // batches: at most max_items_per_batch items, and at least one per lane; n_frames > 1 (the passes of one
+    // multi-pass stream, one after the other): every frame whole batches of the same size
     uint32_t spb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(N, s->max_items_per_batch / n_pix));
     spb = std::min(spb, std::max<uint32_t>(1, (N + want_lanes - 1) / want_lanes));
+    if (n_frames > 1)
+        while (N % spb) --spb;
     f.B = n_pix * spb;
-    f.n_batches = (N + spb - 1) / spb;
+    f.nbpf = (N + spb - 1) / spb;
+    f.n_batches = f.nbpf * n_frames;
     f.lanes = std::max<uint32_t>(1, std::min(want_lanes, f.n_batches));
     f.lane.resize(f.lanes);
-    const uint64_t total = n_pix * N;
+    const uint64_t frame_items = n_pix * N;
     for (uint32_t k = 0; k < f.n_batches; ++k) {
         LaneSched& L = f.lane[k % f.lanes];
         L.batch.push_back(k);
-        const uint64_t nb = std::min(f.B, total - (uint64_t)k * f.B);
+        const uint64_t nb = std::min(f.B, frame_items - (uint64_t)(k % f.nbpf) * f.B);
         L.total += nb;
         L.last_nb = nb;
     }
@@ -1588,7 +1596,7 @@ struct Pending {
     int kind = 0;                   // 0 megakernel, 1 bounce-synchronous wavefront, 2 streaming wavefront
     bool timed = false;             // per-kernel events; the frame runs alone
     bool counted = false;           // the queue counters are kept for render_finish (statistics)
-    uint32_t n_pix = 0, N = 0, depth = 0, n_batches = 0, path_launches = 0;
+    uint32_t n_pix = 0, N = 0, depth = 0, n_batches = 0, path_launches = 0, n_frames = 1;
     uint64_t n_chunks_total = 0;
     std::vector<LaneSched> lanes;               // streaming: the lanes' schedules
     std::vector<std::vector<uint32_t>> inj;     // streaming: camera samples injected per lane and iteration
@@ -1683,10 +1691,15 @@ InjParams inj_params(const FrameSched& f, const LaneSched& ln, uint64_t t) {
         I.jb0 = (uint32_t)(j0 - m * f.B);
         I.nb0 = (uint32_t)ln.nb(m);
         I.nb1 = m + 1 < ln.batch.size() ? (uint32_t)ln.nb(m + 1) : 0u;
-        I.g0 = (uint64_t)k * f.B;
-        I.g1 = m + 1 < ln.batch.size() ? (uint64_t)ln.batch[m + 1] * f.B : 0u;
+        I.g0 = (uint64_t)(k % f.nbpf) * f.B;
+        I.key0 = f.keys[k / f.nbpf];
         I.rad0 = (uint32_t)((k % f.ring) * f.B);
-        I.rad1 = m + 1 < ln.batch.size() ? (uint32_t)((ln.batch[m + 1] % f.ring) * f.B) : 0u;
+        if (m + 1 < ln.batch.size()) {
+            const uint32_t k1 = ln.batch[m + 1];
+            I.g1 = (uint64_t)(k1 % f.nbpf) * f.B;
+            I.key1 = f.keys[k1 / f.nbpf];
+            I.rad1 = (uint32_t)((k1 % f.ring) * f.B);
+        }
     }
     return I;
 }
@@ -1695,9 +1708,14 @@ InjParams inj_params(const FrameSched& f, const LaneSched& ln, uint64_t t) {
 // wavefront (streaming or bounce-synchronous) or megakernel -> ordered accumulation -> into_color into
 // d_out (W*H RGBA on R's device), the last step on `S`, the stream the frame ends on. The path work
 // runs on one of R's frame slots. Nothing here waits for the device.
+// n_frames > 1 (streaming scene modes, no mask): the passes st->pass + f, f < n_frames, of the frame as one sample
+// stream -- pass f + 1's camera samples enter the path pool while pass f's paths drain -- into outs[f] (d_out
+// unused); every frame is the one a call for its pass alone renders (the samples' keys, rad slots and the
+// accumulation order are the same). The frames before the last are written from the slot's accumulate stream,
+// after `outs_after` (the caller's work on S before the call).
 void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, const rs_render_settings* st,
                     RowSet rows, const uint8_t* d_mask, float* d_out, hipStream_t S, Pending& P, bool timed,
-                    bool counted) {
+                    bool counted, uint32_t n_frames = 1, float* const* outs = nullptr, hipEvent_t outs_after = nullptr) {
     P.R = &R;
     P.stream = S;
     P.timed = timed;
@@ -1727,6 +1745,8 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
 
     const bool wavefront = st->mode != RS_MODE_MEGAKERNEL;
     const bool streaming = wavefront && streaming_mode(s->scene_mode);
+    if (n_frames > 1 && (!streaming || d_mask || !outs || !outs_after))
+        throw Error(RS_E_INVALID, "multi-pass stream: streaming scenes, no mask");
     const uint32_t W = cam->width, H = cam->height;
     const uint32_t n_pix = (uint32_t)((uint64_t)n_rows * W);
     const uint32_t sq = (uint32_t)std::floor(std::sqrt((double)st->samples));  // painter.rs:110-118
@@ -1779,7 +1799,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     } else if (streaming) {
         const uint32_t want = ext_spill ? 1u : std::min<uint32_t>(kMaxLanes, s->stream_lanes);
         uint64_t pool = pool_limit(s, R, want);
-        FrameSched f = make_sched(s, n_pix, N, D, want, pool);
+        FrameSched f = make_sched(s, n_pix, N, D, want, pool, n_frames);
         auto rad_n = [&]() { return (size_t)3 * f.ring * f.B; };
         // the smallest pool a frame is scheduled on: 64 Ki camera samples per iteration (or the whole frame); below
         // that the iterations (and their counter blocks) multiply, and the render reports the device as full
@@ -1787,15 +1807,18 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         if (f.cap > L.wf_cap || f.lanes > L.wf_lanes || rad_n() > L.rad_cap) {
             // the slot allocates: as much as the device has free
             const uint64_t fp = std::max(pool_min, pool_limit_free(s, R, L, want, rad_n() * sizeof(double)));
-            if (fp < pool) { pool = fp; f = make_sched(s, n_pix, N, D, want, pool); }
+            if (fp < pool) { pool = fp; f = make_sched(s, n_pix, N, D, want, pool, n_frames); }
         }
         // an allocation that still fails (memory taken meanwhile): both buffers back, half the pool
         while (!carve_wf(L, f.cap, f.lanes) || !try_ensure(L, L.d_rad, L.rad_cap, rad_n())) {
             release_pool(L);
             if (pool <= pool_min) throw Error(RS_E_NOMEM, "device memory exhausted: no room for the frame's path pool");
             pool = std::max<uint64_t>(pool_min, pool / 2);
-            f = make_sched(s, n_pix, N, D, want, pool);
+            f = make_sched(s, n_pix, N, D, want, pool, n_frames);
         }
+        f.keys.resize(n_frames);
+        for (uint32_t k = 0; k < n_frames; ++k)
+            f.keys[k] = splitmix64_h(splitmix64_h(st->seed) ^ (uint64_t)(st->pass + k));
         n_counts = f.n_counts;
         uint32_t* const prev_counts = L.d_counts;
         ensure(L, L.d_counts, L.counts_cap, n_counts);
@@ -1810,6 +1833,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         HIP_OK(hipEventRecord(L.fork_ev, L0));
         for (uint32_t l = 1; l < f.lanes; ++l) HIP_OK(hipStreamWaitEvent(ls[l], L.fork_ev, 0));
         HIP_OK(hipStreamWaitEvent(L.acc_stream, L.fork_ev, 0));
+        if (n_frames > 1) HIP_OK(hipStreamWaitEvent(L.acc_stream, outs_after, 0));
         // per batch: its paths are done (recorded on its lane) / it has been accumulated (acc stream)
         while (L.bev.size() < 2 * (size_t)f.n_batches) {
             hipEvent_t e;
@@ -1818,7 +1842,9 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         }
         auto done_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k]; };
         auto acc_ev = [&](uint32_t k) { return L.bev[2 * (size_t)k + 1]; };
-        const bool split = ext_split(sm) || s->ext_split;
+        // (a multi-pass stream's iterations carry paths and inject camera samples: two launches, each part at its own
+        // occupancy -- 30 share frames of the bench frame 0.971 -> 0.909 ms, profiles/r6/passes)
+        const bool split = ext_split(sm) || s->ext_split || n_frames > 1;
         // lean / heavy shading launches (spheres mode; nest modes with an LDS image) pay one more launch tail per
         // iteration: worth it on full frames (bench 7.16 -> 7.09 ms), not on small ones (the N = 8 row share, 3.2 M
         // samples: 1.013 -> 1.066 ms)
@@ -1906,13 +1932,16 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
              },
              [&](uint32_t k) {
                  // batch k's samples have all finished: accumulate in sample order (the last batch on S,
-                 // writing the frame and zeroing the counters for the next frame unless statistics read them)
-                 const uint32_t planes = (uint32_t)(std::min<uint64_t>(f.B, (uint64_t)n_pix * N - (uint64_t)k * f.B) / n_pix);
+                 // writing the frame and zeroing the counters for the next frame unless statistics read them;
+                 // an earlier pass's last batch into its frame, on the accumulate stream)
+                 const uint32_t fr = k / f.nbpf, kl = k % f.nbpf;
+                 float* const out = n_frames > 1 ? outs[fr] : d_out;
+                 const uint32_t planes = (uint32_t)(std::min<uint64_t>(f.B, (uint64_t)n_pix * N - (uint64_t)kl * f.B) / n_pix);
                  const double* rk = L.d_rad + (size_t)3 * (k % f.ring) * f.B;  // item-major radiance (put_rad)
                  if (k + 1 < f.n_batches) {
                      HIP_OK(hipStreamWaitEvent(L.acc_stream, done_ev(k), 0));
-                     HIP_OK(launch_accumulate(rk, L.d_acc, n_pix, planes, k == 0, 0, fp, d_out, nullptr, 0,
-                                              L.acc_stream));
+                     HIP_OK(launch_accumulate(rk, L.d_acc, n_pix, planes, kl == 0, kl + 1 == f.nbpf ? 1 : 0, fp, out,
+                                              nullptr, 0, L.acc_stream));
                      HIP_OK(hipEventRecord(acc_ev(k), L.acc_stream));
                  } else {
                      HIP_OK(hipEventRecord(L.join_ev[0], L.acc_stream));
@@ -1925,7 +1954,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      HIP_OK(hipEventRecord(L.fork_ev, L0));
                      HIP_OK(hipStreamWaitEvent(S, L.fork_ev, 0));
                      const size_t nz = counted ? 0 : n_counts;
-                     HIP_OK(launch_accumulate(rk, L.d_acc, n_pix, planes, k == 0, 1, fp, d_out, L.d_counts,
+                     HIP_OK(launch_accumulate(rk, L.d_acc, n_pix, planes, kl == 0, 1, fp, out, L.d_counts,
                                               (uint32_t)nz, S));
                      L.counts_clean = nz;
                  }
@@ -2057,6 +2086,7 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
     HIP_OK(hipEventRecord(L.free_ev, S));
     L.free_rec = true;
     P.kind = !wavefront ? 0 : streaming ? 2 : 1;
+    P.n_frames = n_frames;
     P.n_pix = n_pix;
     P.N = N;
     P.depth = D;
@@ -2094,7 +2124,7 @@ void render_finish(const rs_scene* s, Pending& P, rs_render_stats* stats) {
         HIP_OK(hipEventElapsedTime(&ms, P.kev[2 * k], P.kev[2 * k + 1]));
         kernel_ms += ms;
     }
-    const uint64_t items = (uint64_t)P.n_pix * P.N;
+    const uint64_t items = (uint64_t)P.n_pix * P.N * P.n_frames;
     uint64_t seg = 0, kbytes = 0;
     if (P.kind == 0) {
         for (int i = 0; i < 256; ++i) seg += P.cnt[i];
@@ -2243,6 +2273,81 @@ void render_frame_device(rs_scene* s, const rs_camera_desc* cam, const rs_render
     }
     for (hipEvent_t e : done) if (e) (void)hipEventDestroy(e);
     if (entry) (void)hipEventDestroy(entry);
+    acc.tree_arity = s->tree_arity;
+    acc.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = acc;
+}
+
+// rs_render_device_passes: passes st->pass + k into d_outs[k]. One replica, a streaming scene mode and a pass the
+// stream pays for: multi-pass sample streams (render_enqueue's n_frames); otherwise a render_frame_device per pass.
+// Measured, 30 passes of RTIOW per call against 30 asynchronous one-pass calls (ms per pass, profiles/r6/passes):
+//   800x500x64 depth 8: 6.39 / 6.52 (stream), its rows 0::8 0.891 / 0.919; 400x250x16 0.492 / 0.502, rows 0::8
+//   0.163 / 0.139; 200x125x16 0.202 / 0.197, rows 0::8 0.136 / 0.104; depth 50: 800x500x64 7.84 / 8.04, rows 0::8
+//   1.256 / 1.064 -- the stream pays where a pass's late iterations are a large part of its time (small passes, or
+//   deep ones of a few million samples), and costs 2-3 % on passes that fill the GPU by themselves.
+bool passes_stream_pays(uint64_t items, uint32_t depth) {
+    return items <= (1ull << 20) || (depth >= 16 && items <= (8ull << 20));
+}
+void render_passes_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, uint32_t n,
+                          float* const* d_outs, hipStream_t stream, rs_render_stats* stats) {
+    if (n && !d_outs) throw Error(RS_E_INVALID, "null argument");
+    for (uint32_t k = 0; k < n; ++k)
+        if (!d_outs[k]) throw Error(RS_E_INVALID, "null argument");
+    validate_render(s, cam, st);
+    const auto t0 = std::chrono::steady_clock::now();
+    rs_render_stats acc{};
+    const uint32_t sq = (uint32_t)std::floor(std::sqrt((double)st->samples));
+    const RowSet rows = replica_rows(cam, st, 0, 1);
+    const bool stream_all = n > 1 && s->reps.size() == 1 && st->mode != RS_MODE_MEGAKERNEL &&
+                            streaming_mode(s->scene_mode) && sq > 0 && rows.count() > 0 &&
+                            s->passes_stream != 2 &&
+                            (s->passes_stream == 1 ||
+                             passes_stream_pays((uint64_t)rows.count() * cam->width * sq * sq, st->depth));
+    if (!stream_all) {
+        for (uint32_t k = 0; k < n; ++k) {
+            rs_render_settings sk = *st;
+            sk.pass = st->pass + k;
+            rs_render_stats one{};
+            render_frame_device(s, cam, &sk, nullptr, d_outs[k], stream, stats ? &one : nullptr);
+            acc.samples += one.samples; acc.segments += one.segments; acc.path_ms += one.path_ms;
+            acc.launches += one.launches; acc.kernel_launches += one.kernel_launches; acc.kernel_ms += one.kernel_ms;
+            acc.kernel_bytes += one.kernel_bytes; acc.kernel_id = one.kernel_id;
+        }
+    } else {
+        // contiguous groups of passes, one per frame slot, streamed concurrently (a single sample stream is one chain
+        // of dependent launches: 12 share frames of the bench frame took 1.01 ms each as one stream, 1.25 as one-pass
+        // frames on one slot, 0.885 as one-pass frames over three slots; profiles/r6/passes); one group when an
+        // output pointer repeats (later passes overwrite earlier ones: their writes stay in pass order)
+        Replica& R = *s->reps[0];
+        DeviceGuard g(R.device);
+        uint32_t groups = std::min<uint32_t>(frame_slots(s), n);
+        {
+            std::vector<float*> sorted(d_outs, d_outs + n);
+            std::sort(sorted.begin(), sorted.end());
+            if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) groups = 1;
+        }
+        std::vector<std::unique_ptr<Pending>> P(groups);
+        hipEvent_t entry = nullptr;  // the caller's work on `stream` before the call: the earlier frames' writes wait
+        try {
+            HIP_OK(hipEventCreateWithFlags(&entry, hipEventDisableTiming));
+            HIP_OK(hipEventRecord(entry, stream));
+            for (uint32_t k = 0; k < groups; ++k) {
+                const uint32_t lo = (uint32_t)((uint64_t)n * k / groups), hi = (uint32_t)((uint64_t)n * (k + 1) / groups);
+                rs_render_settings sg = *st;
+                sg.pass = st->pass + lo;
+                P[k].reset(new Pending());
+                render_enqueue(s, R, cam, &sg, rows, nullptr, d_outs[lo], stream, *P[k], stats != nullptr, false,
+                               hi - lo, d_outs + lo, entry);
+                if (stats) render_finish(s, *P[k], &acc);
+            }
+            if (stats) HIP_OK(hipStreamSynchronize(stream));
+        } catch (...) {
+            (void)hipDeviceSynchronize();  // drain what was enqueued before the buffers go away
+            if (entry) (void)hipEventDestroy(entry);
+            throw;
+        }
+        HIP_OK(hipEventDestroy(entry));
+    }
     acc.tree_arity = s->tree_arity;
     acc.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (stats) *stats = acc;
@@ -2450,6 +2555,7 @@ int rs_scene_create(rs_scene** out) {
         v = 0; knob("RS_EXT_SPLIT", v); s->ext_split = v != 0;
         v = 0; knob("RS_SHADE_MERGED", v); if (v) s->shade_split = false;
         v = 0; knob("RS_DUMP_ITERS", v); s->dump_iters = v != 0;
+        v = 0; knob("RS_PASSES_STREAM", v); s->passes_stream = (uint32_t)v;
 #endif
         *out = s;
     });
@@ -2697,6 +2803,13 @@ int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
                      float* d_out, void* stream, rs_render_stats* stats) {
     return run([&] {
         render_frame_device(S(s), cam, st, d_mask, d_out, (hipStream_t)stream, stats);
+    });
+}
+
+int rs_render_device_passes(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, uint32_t n_passes,
+                            float* const* d_outs, void* stream, rs_render_stats* stats) {
+    return run([&] {
+        render_passes_device(S(s), cam, st, n_passes, d_outs, (hipStream_t)stream, stats);
     });
 }
 

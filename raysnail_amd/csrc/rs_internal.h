@@ -128,6 +128,7 @@ struct InjParams {
     uint32_t nb1;         // items in the next batch (0: none)
     uint64_t g0, g1;      // frame items of the two batches' starts (k * batch: a lane's batches are not adjacent)
     uint32_t rad0, rad1;  // rad ring offsets of the two batches' buffers
+    uint64_t key0, key1;  // the two batches' PathParams::key_base (a multi-pass stream: their passes' keys)
 };
 
 struct FinalParams {

@@ -1264,10 +1264,10 @@ __device__ __forceinline__ uint32_t block_slot1(bool flag, uint32_t* counter) {
 // painter.rs:167-170 + camera.rs:77-85 for every (pixel, sample) item of a chunk
 // Camera sample `item` of the batch (painter.rs:154-187 jitter, camera.rs:77-85 ray): false for a
 // masked pixel (painter.rs:204-210) or depth 0 (camera.rs:161), whose radiance is 0.
-__device__ __forceinline__ void camera_sample_xy(const DCamera& C, const PathParams& P, uint32_t x, uint32_t y,
-                                                 uint32_t s, Ray& r, Rng& rng) {
+__device__ __forceinline__ void camera_sample_xy(const DCamera& C, const PathParams& P, uint64_t key, uint32_t x,
+                                                 uint32_t y, uint32_t s, Ray& r, Rng& rng) {
     const uint64_t pix = (uint64_t)y * P.width + x;
-    rng.seed_from_u64(splitmix64(splitmix64(P.key_base ^ pix) ^ (uint64_t)s));
+    rng.seed_from_u64(splitmix64(splitmix64(key ^ pix) ^ (uint64_t)s));
     const uint32_t si = s % P.sqrt_spp, sj = s / P.sqrt_spp;
     const double sq = (double)P.sqrt_spp;
     const double xo = (double)x + ((double)si + rng.gen()) / sq;
@@ -1275,15 +1275,19 @@ __device__ __forceinline__ void camera_sample_xy(const DCamera& C, const PathPar
     const double hh = (double)P.height;
     r = camera_ray(C, xo / (double)P.width, (hh - 1.0 - yo) / hh, rng);
 }
-__device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
+__device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams& P, uint64_t key, uint64_t item, Ray& r,
+                                              Rng& rng) {
     const uint32_t pl = (uint32_t)(item % P.n_pix_local);
     const uint32_t sl = (uint32_t)(item / P.n_pix_local);
     const uint32_t x = pl % P.width;
     const uint32_t y = P.row_begin + (pl / P.width) * P.row_step;
     const uint64_t pix = (uint64_t)y * P.width + x;
     if ((P.mask && !P.mask[pix]) || P.depth == 0) return false;
-    camera_sample_xy(C, P, x, y, P.s0 + sl, r, rng);
+    camera_sample_xy(C, P, key, x, y, P.s0 + sl, r, rng);
     return true;
+}
+__device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams& P, uint64_t item, Ray& r, Rng& rng) {
+    return camera_sample(C, P, P.key_base, item, r, rng);
 }
 
 // Camera-ray order: the i-th camera sample a launch traces is item gen_perm(i) of its batch (whole
@@ -1326,13 +1330,14 @@ __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_
 }
 
 // The camera sample behind the streaming iteration's injected record jg (0-based among its injections):
-// its frame item g (camera_sample) and its radiance slot in the rad ring.
+// its frame item g (camera_sample), its pass's key and its radiance slot in the rad ring.
 __device__ __forceinline__ void inj_sample(const InjParams& I, const PathParams& P, uint32_t jg, uint64_t& g,
-                                           uint32_t& item) {
+                                           uint64_t& key, uint32_t& item) {
     uint32_t jb = I.jb0 + jg, nb = I.nb0;
     uint64_t g0 = I.g0;
     item = I.rad0;
-    if (jb >= I.nb0) { jb -= I.nb0; nb = I.nb1; g0 = I.g1; item = I.rad1; }
+    key = I.key0;
+    if (jb >= I.nb0) { jb -= I.nb0; nb = I.nb1; g0 = I.g1; item = I.rad1; key = I.key1; }
     const uint32_t perm = gen_perm(jb, 0, nb, P);
     item += perm;
     g = g0 + perm;
@@ -1725,9 +1730,9 @@ __global__ __launch_bounds__(kBlock, ext_min_waves(SM, LOBJ, PART)) void k_wfs_e
         uint32_t item = 0;
         if (j < n) {
             if (gen) {
-                uint64_t g;
-                inj_sample(I, P, j - n_old, g, item);
-                live = camera_sample(C, P, g, r, rng);
+                uint64_t g, key;
+                inj_sample(I, P, j - n_old, g, key, item);
+                live = camera_sample(C, P, key, g, r, rng);
                 if (!live) put_rad(rad, item, 0.0, 0.0, 0.0);
             } else {
                 r = load_ray(cur, i, W.tagw);
@@ -2156,7 +2161,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_sample(const DScene* __restric
     if (i >= n) return;
     Ray r;
     Rng rng;
-    camera_sample_xy(C, P, x, y, s0 + i, r, rng);
+    camera_sample_xy(C, P, P.key_base, x, y, s0 + i, r, rng);
     uint32_t segs = 0;
     const V3 L = trace_path<SM>(S, r, P.depth, rng, make_stk(S, stk_all), segs);
     out[4 * (size_t)i] = L.x; out[4 * (size_t)i + 1] = L.y; out[4 * (size_t)i + 2] = L.z;

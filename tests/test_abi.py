@@ -24,7 +24,7 @@ def test_header_lists_all_exports():
 def test_library_exports_every_declared_symbol(hip_lib):
     for name in header_symbols():
         assert hasattr(hip_lib, name), name
-    assert hip_lib.rs_abi_version() == 5
+    assert hip_lib.rs_abi_version() == 6
 
 
 def _scene(lib):
@@ -226,13 +226,20 @@ def _c_param_type(decl):
     arr = re.search(r"\[\d+\]\s*$", decl)
     decl = re.sub(r"\[\d+\]\s*$", "", decl)
     toks = decl.replace("*", " * ").split()
-    const = toks[0] == "const"
+    const = toks[0] == "const"  # `const` qualifies what is to its left (the base type when it leads)
     if const:
         toks = toks[1:]
-    stars = toks.count("*") + (1 if arr else 0)
     t = base[toks[0]]
-    for k in range(stars):
-        t = ("*const " if (const and k == 0) else "*mut ") + t
+    rest = toks[1:]
+    if rest and rest[0] == "const":
+        const, rest = True, rest[1:]
+    for k, tok in enumerate(rest):
+        if tok != "*":
+            continue
+        t = ("*const " if const else "*mut ") + t
+        const = k + 1 < len(rest) and rest[k + 1] == "const"  # `T* const*`: the outer pointer's pointee is const
+    if arr:
+        t = ("*const " if const else "*mut ") + t
     return t
 
 

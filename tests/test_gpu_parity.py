@@ -568,3 +568,57 @@ def test_deep_spheres_stack_spill_matches_oracle(gpu):
     ref, rs = _oracle(world).render(cam.desc, st)
     assert stats.segments == rs.segments
     assert np.array_equal(img, ref)
+
+
+@pytest.mark.parametrize("name", ["rtow", "example_sdl", "quadric_sdl", "mesh"])
+def test_render_device_passes_stream(gpu, name):
+    """rs_render_device_passes: n progressive passes of one frame (raysnail.rs:379-427's pass loop) as one sample
+    stream -- pass k + 1's camera samples enter the pool while pass k's paths drain -- equal, frame by frame, the
+    passes rendered one call each, and pass 0 equals the oracle's. Pools from whole passes down to 256 samples per
+    iteration and radiance batches of 1-16 sample planes (a pass is several batches; several passes' batches in the
+    ring at once), one and two lanes, repeated output pointers, a row share (rows 1::4), and the statistics summed
+    over the passes. `mesh` (bounce-synchronous) takes the one-call-per-pass fallback."""
+    torch = gpu
+    build = {"rtow": lambda: scenes.rtow_13_1(64, 40)[:2], "example_sdl": lambda: scenes.example_sdl(64, 40),
+             "quadric_sdl": lambda: scenes.quadric_sdl(48, 48), "mesh": lambda: scenes.mesh_scene(64, 36, 24, 60)}[name]
+    cam, world = build()
+    H, W = cam.desc.height, cam.desc.width
+    ds = world.device_scene()
+    s = torch.cuda.current_stream().cuda_stream
+    n = 5
+    for rows in ((0, 0, 1), (1, 0, 4)):
+        photo = cam.take_photo().samples(16).depth(10).seed(8).pass_index(3).rows(*rows)
+        st = photo.settings()
+        singles = []
+        one_stats = []
+        for k in range(n):
+            o = torch.full((H, W, 4), -1.0, dtype=torch.float32, device="cuda")
+            one_stats.append(ds.render_device(cam.desc, cam.take_photo().samples(16).depth(10).seed(8)
+                                              .pass_index(3 + k).rows(*rows).settings(), o.data_ptr(), s))
+            singles.append(o.cpu().numpy())
+        if rows == (0, 0, 1):
+            ref, rs = _oracle(world).render(cam.desc, st, threads=16)
+            assert np.array_equal(singles[0], ref)
+        npx = W * len(range(rows[0], H, rows[2]))
+        for batch, pool in ((32 << 20, 16 << 20), (npx, 256 * 10), (4 * npx, 7000), (16 * npx, 3 * 16 * npx)):
+            ds.set_workspace(batch, pool)
+            for lanes in (1, 2):
+                ds.set_lanes(lanes)
+                outs = [torch.full((H, W, 4), -1.0, dtype=torch.float32, device="cuda") for _ in range(n)]
+                stats = ds.render_device_passes(cam.desc, st, [o.data_ptr() for o in outs], s)
+                for k in range(n):
+                    assert np.array_equal(outs[k].cpu().numpy(), singles[k]), (name, rows, batch, pool, lanes, k)
+                assert stats.samples == sum(x.samples for x in one_stats)
+                assert stats.segments == sum(x.segments for x in one_stats), (name, rows, batch, pool, lanes)
+                # asynchronous, two outputs reused (later passes overwrite), back to back with a one-pass call
+                pair = [torch.full((H, W, 4), -1.0, dtype=torch.float32, device="cuda") for _ in range(2)]
+                assert ds.render_device_passes(cam.desc, st, [pair[k % 2].data_ptr() for k in range(n)], s,
+                                               stats=False) is None
+                last = torch.full((H, W, 4), -1.0, dtype=torch.float32, device="cuda")
+                ds.render_device_passes(cam.desc, st, [last.data_ptr()], s, stats=False)
+                torch.cuda.synchronize()
+                assert np.array_equal(pair[(n - 1) % 2].cpu().numpy(), singles[n - 1])
+                assert np.array_equal(pair[(n - 2) % 2].cpu().numpy(), singles[n - 2])
+                assert np.array_equal(last.cpu().numpy(), singles[0])
+        ds.set_workspace(32 << 20, 256 << 20)
+        ds.set_lanes(0)

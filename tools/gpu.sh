@@ -195,6 +195,24 @@ for s in "$@"; do
       (cd /tmp && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_DUMP_ITERS=1 step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/iters_$1 -o it -- python3 $R/tools/render_once.py 0 4 $1 $2 $3 > $OUT/iters_$1.log 2>&1) || { echo "iters trace $1 failed"; tail -5 $OUT/iters_$1.log; exit 1; }
       (cd $R && python3 tools/iter_table.py $OUT/iters_$1.log $(ls $OUT/iters_$1/*kernel_trace.csv) | tee $OUT/iters_$1.txt)
     done ;;
+  passtest)
+    (cd $R && step 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "passes or streaming_pool or queue_counter" > $OUT/pytest_passes.log 2>&1) || { echo "passes tests failed"; tail -30 $OUT/pytest_passes.log; exit 1; }
+    tail -1 $OUT/pytest_passes.log ;;
+  passes)
+    # rs_render_device_passes (K passes as one sample stream) against K pipelined one-pass frames: bench frame, N = 8 share
+    # PASSARGS="...;...": one probe run per entry (default the bench frame and its N = 8 share)
+    IFS=';' read -ra PA <<< "${PASSARGS:- }"
+    for a in "${PA[@]}"; do
+      (cd $R && step 300 python3 tools/passes_probe.py $a >> $OUT/passes.jsonl 2>> $OUT/passes.err) || { echo "passes probe failed"; tail -5 $OUT/passes.err; exit 1; }
+    done
+    cat $OUT/passes.jsonl ;;
+  passtrace)
+    # kernel traces of K = 12 row-share frames, one call per pass against the passes stream (one lane, one slot)
+    for m in single stream; do
+      (cd /tmp && step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/pt_$m -o t -- python3 $R/tools/passes_trace.py $m 12 ${PT_ROWSTEP:-8} > $OUT/pt_$m.log 2>&1) || { echo "passes trace $m failed"; tail -5 $OUT/pt_$m.log; exit 1; }
+      (cd $R && echo "== $m" >> $OUT/passtrace.txt && python3 tools/trace_sum.py $(ls $OUT/pt_$m/*kernel_trace.csv) 12 >> $OUT/passtrace.txt)
+    done
+    cat $OUT/passtrace.txt ;;
   configs)
     (cd $R && step 900 python3 tools/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err) || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
     cat $OUT/configs.jsonl ;;
