@@ -213,6 +213,21 @@ for s in "$@"; do
       (cd $R && echo "== $m" >> $OUT/passtrace.txt && python3 tools/trace_sum.py $(ls $OUT/pt_$m/*kernel_trace.csv) 12 >> $OUT/passtrace.txt)
     done
     cat $OUT/passtrace.txt ;;
+  abenv)
+    # this build's bench line against the dev library with ABENV (a dev knob that turns a feature off), 3 rounds
+    B="--cpu-baseline 0 --steps 20 --warmup 5"
+    for rep in 1 2 3; do
+      (cd $R && step 240 env RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so $ABENV python3 bench.py $B > $OUT/abenv_off_$rep.json 2> $OUT/abenv.err) || { echo "dev bench failed"; tail -5 $OUT/abenv.err; exit 1; }
+      (cd $R && step 240 python3 bench.py $B > $OUT/abenv_on_$rep.json 2> $OUT/abenv.err) || { echo "bench failed"; tail -5 $OUT/abenv.err; exit 1; }
+    done
+    (cd $R && python3 tools/ab_report.py $OUT/abenv_off_*.json -- $OUT/abenv_on_*.json | tee $OUT/abenv.txt) ;;
+  envtrace)
+    # kernel traces of 4 bench frames (tools/render_once.py): the dev library with ABENV, then this build; per-kernel
+    # time per frame of the last two (tools/trace_sum.py)
+    (cd /tmp && step 200 env RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so $ABENV rocprofv3 --kernel-trace --output-format csv -d $OUT/et_off -o t -- python3 $R/tools/render_once.py 0 4 > $OUT/et_off.log 2>&1) || { echo "env trace failed"; tail -5 $OUT/et_off.log; exit 1; }
+    (cd /tmp && step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/et_on -o t -- python3 $R/tools/render_once.py 0 4 > $OUT/et_on.log 2>&1) || { echo "trace failed"; tail -5 $OUT/et_on.log; exit 1; }
+    for m in off on; do (cd $R && echo "== $m" >> $OUT/envtrace.txt && python3 tools/trace_sum.py $(ls $OUT/et_$m/*kernel_trace.csv) 2 >> $OUT/envtrace.txt); done
+    cat $OUT/envtrace.txt ;;
   configs)
     (cd $R && step 900 python3 tools/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err) || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
     cat $OUT/configs.jsonl ;;
