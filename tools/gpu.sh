@@ -228,6 +228,16 @@ for s in "$@"; do
     (cd /tmp && step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/et_on -o t -- python3 $R/tools/render_once.py 0 4 > $OUT/et_on.log 2>&1) || { echo "trace failed"; tail -5 $OUT/et_on.log; exit 1; }
     for m in off on; do (cd $R && echo "== $m" >> $OUT/envtrace.txt && python3 tools/trace_sum.py $(ls $OUT/et_$m/*kernel_trace.csv) 2 >> $OUT/envtrace.txt); done
     cat $OUT/envtrace.txt ;;
+  libtrace)
+    # kernel traces of 4 bench frames (tools/render_once.py) with the product and every variant; per-kernel time per
+    # frame of the last two (tools/trace_sum.py)
+    for v in $R/raysnail_amd/lib/libraysnail_hip.so $R/raysnail_amd/lib/var_*.so; do
+      [ -e "$v" ] || continue
+      n=$(basename $v .so)
+      (cd /tmp && RS_HIP_LIB=$v step 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/lt_$n -o t -- python3 $R/tools/render_once.py 0 4 > $OUT/lt_$n.log 2>&1) || { echo "lib trace $n failed"; tail -5 $OUT/lt_$n.log; exit 1; }
+      (cd $R && echo "== $n" >> $OUT/libtrace.txt && python3 tools/trace_sum.py $(ls $OUT/lt_$n/*kernel_trace.csv) 2 >> $OUT/libtrace.txt)
+    done
+    cat $OUT/libtrace.txt ;;
   configs)
     (cd $R && step 900 python3 tools/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err) || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
     cat $OUT/configs.jsonl ;;
