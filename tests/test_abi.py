@@ -60,6 +60,13 @@ def test_render_before_commit_is_state_error(hip_lib):
     import numpy as np
     out = np.zeros((4, 4, 4), np.float32)
     assert lib.rs_render(s, C.byref(cam), C.byref(st), None, out.ctypes.data, None) == A.RS_E_STATE
+    # rs_render_device_passes: argument checks before any device work (no GPU needed)
+    ptrs = (C.c_void_p * 2)(C.c_void_p(0x1000), C.c_void_p(0x2000))
+    assert lib.rs_render_device_passes(s, C.byref(cam), C.byref(st), 2, ptrs, None, None) == A.RS_E_STATE
+    assert lib.rs_render_device_passes(None, C.byref(cam), C.byref(st), 2, ptrs, None, None) == A.RS_E_INVALID
+    assert lib.rs_render_device_passes(s, C.byref(cam), C.byref(st), 2, None, None, None) == A.RS_E_INVALID
+    holes = (C.c_void_p * 2)(C.c_void_p(0x1000), None)
+    assert lib.rs_render_device_passes(s, C.byref(cam), C.byref(st), 2, holes, None, None) == A.RS_E_INVALID
     lib.rs_scene_destroy(s)
 
 

@@ -126,3 +126,24 @@ def test_host_only_commit_refuses_render(gpu):
     assert ds.info().n_devices == 0
     with pytest.raises(api.RaysnailError):
         ds.render(cam.desc, cam.take_photo().samples(1).settings())
+
+
+def test_virtual_devices_render_device_passes(gpu):
+    """rs_render_device_passes on a scene committed to virtual devices {0, 0} (one-pass calls over the devices) and
+    on one device with passes too large for the sample stream (1.2 M samples at depth 8: one-pass calls): every pass
+    equals its one-pass frame on one device."""
+    torch = gpu
+    s = torch.cuda.current_stream().cuda_stream
+    for w, h, spp, devs in ((64, 40, 4, [0, 0]), (1200, 1000, 1, [0])):
+        cam, world, _, _ = scenes.rtow_13_1(w, h)
+        one = api.DeviceScene(world, devices=[0])
+        ds = api.DeviceScene(world, devices=devs)
+        photo = cam.take_photo().samples(spp).depth(8).seed(9).pass_index(5)
+        outs = [torch.full((h, w, 4), -1.0, dtype=torch.float32, device="cuda") for _ in range(3)]
+        stats = ds.render_device_passes(cam.desc, photo.settings(), [o.data_ptr() for o in outs], s)
+        assert stats.samples == 3 * w * h * spp
+        for k in range(3):
+            ref = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+            one.render_device(cam.desc, cam.take_photo().samples(spp).depth(8).seed(9).pass_index(5 + k).settings(),
+                              ref.data_ptr(), s)
+            assert np.array_equal(outs[k].cpu().numpy(), ref.cpu().numpy(), equal_nan=True), (w, devs, k)
