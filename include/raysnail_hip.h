@@ -330,13 +330,15 @@ int rs_render_device(rs_scene* s, const rs_camera_desc* cam, const rs_render_set
                      const uint8_t* d_mask, float* d_out_rgba, void* stream, rs_render_stats* stats);
 /* n_passes progressive passes of one frame into device frames: pass st->pass + k into d_outs[k] (k < n_passes;
  * the pointers may repeat: later passes overwrite), each frame bitwise the one rs_render_device renders for that
- * pass (no mask: the CLI's pass loop with its never-applied redo map, src/bin/raysnail.rs:379-427). Streaming
- * scene modes (spheres, box / CSG: rs_scene_info.scene_mode 1, 3, 4) on one device run the passes as one sample
- * stream: pass k + 1's camera samples enter the path pool while pass k's paths drain, so the small late launches of
- * a pass are filled with the next one's work (a frame's share of a strong-scaled multi-GPU render is a few million
- * samples); other scenes and several devices render the passes one rs_render_device call after the other. Stream
- * and stats semantics as rs_render_device (stats summed over the passes). No reference counterpart as one call:
- * the reference renders its passes one after the other (raysnail.rs:379). */
+ * pass (no mask: the CLI's pass loop with its never-applied redo map, src/bin/raysnail.rs:379-427). On one device,
+ * in the streaming scene modes (spheres, box / CSG: rs_scene_info.scene_mode 1, 3, 4), passes of at most 1 Mi
+ * samples -- or 8 Mi at depth >= 16 -- run as sample streams, one per frame slot over a contiguous group of the
+ * passes: pass k + 1's camera samples enter the path pool while pass k's paths drain, so the small late launches of
+ * a pass carry the next one's work. A stream's path pool bounds the paths its passes can leave in flight: up to
+ * depth x one pass's samples per slot, within the caps of rs_scene_set_workspace. Everything else renders the
+ * passes one rs_render_device call after the other (larger passes fill the device alone; the stream measured 2-3 %
+ * slower there). Stream and stats semantics as rs_render_device (stats summed over the passes). No reference
+ * counterpart as one call: the reference renders its passes one after the other (raysnail.rs:379). */
 int rs_render_device_passes(rs_scene* s, const rs_camera_desc* cam, const rs_render_settings* st, uint32_t n_passes,
                             float* const* d_outs_rgba, void* stream, rs_render_stats* stats);
 
