@@ -182,6 +182,10 @@ struct Slot {
     size_t counts_clean = 0;  // leading entries of d_counts known to be zero (reset by the last frame's accumulate)
     hipStream_t acc_stream = nullptr;         // streaming wavefront: the batches' accumulates
     std::vector<hipEvent_t> bev;              // per batch: its paths done, its accumulate done
+    // the carried-path counts of the slot's last streaming frame (per lane and iteration), copied into pinned host
+    // memory at its end: they size the carried-extend grids of later frames of the same shape (Replica::hist)
+    uint32_t* h_hist = nullptr; size_t hist_cap = 0, hist_words = 0; uint64_t hist_sig = 0;
+    hipEvent_t hist_ev = nullptr; bool hist_pending = false;
 
     // wait until nothing in flight uses this slot's buffers
     void quiesce() {
@@ -205,6 +209,8 @@ struct Slot {
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : bev) (void)hipEventDestroy(e);
         if (acc_stream) (void)hipStreamDestroy(acc_stream);
+        if (hist_ev) (void)hipEventDestroy(hist_ev);
+        if (h_hist) (void)hipHostFree(h_hist);
     }
 };
 
@@ -223,6 +229,8 @@ struct Replica {
     int32_t* d_ovf = nullptr; size_t ovf_cap = 0;   // traversal-stack overflow (entries beyond the LDS part)
     DScene* d_ds = nullptr;                 // ds in device memory (what the kernels read)
     DScene uploaded{};                      // the copy last written to d_ds
+    std::vector<uint32_t> hist;             // the latest completed streaming frame's carried counts (Slot::h_hist)
+    uint64_t hist_sig = 0;                  // and its schedule's signature
 
     // wait until no frame of this replica is in flight (before a shared buffer is replaced)
     void quiesce() {
@@ -1825,6 +1833,47 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
         if (L.d_counts != prev_counts) L.counts_clean = 0;
         if (n_counts > L.counts_clean) HIP_OK(hipMemsetAsync(L.d_counts, 0, n_counts * sizeof(uint32_t), L0));
         L.counts_clean = 0;
+        // Carried-extend grids. Without history a carried launch takes a block per 256 of the paths injected in the
+        // last depth - 1 iterations (the bound on what it can carry), though from the second bounce on it carries a
+        // few of them (bench frame: 28 % at t = 2, 3 % at t = 7): the empty blocks only read the count and leave, but
+        // their dispatch costs a launch some microseconds. A frame of the same shape as one completed earlier takes
+        // that frame's count of the iteration + 25 % + 16 Ki paths (blocks grid-stride over what exceeds it, so the
+        // frame never depends on the estimate). The counts reach pinned host memory at the end of each frame
+        // (Slot::h_hist) and are read here without waiting (bench frame 6.47 -> 6.39 ms with a fixed cap,
+        // profiles/r6/ab/carried_cap_r6g1.txt).
+        uint64_t sig = splitmix64_h(((uint64_t)n_pix << 32) ^ N) ^ splitmix64_h(((uint64_t)D << 40) ^ ((uint64_t)f.lanes << 32) ^ n_frames);
+        std::vector<size_t> hoff(f.lanes, 0);
+        size_t hwords = 0;
+        for (uint32_t l = 0; l < f.lanes; ++l) {
+            const LaneSched& ln = f.lane[l];
+            sig = splitmix64_h(sig ^ ln.Q ^ (ln.T << 40) ^ (ln.total << 1) ^ (uint64_t)ln.finish);
+            hoff[l] = hwords;
+            hwords += ln.T;
+        }
+        for (Slot& o : R.slots) {
+            if (!o.hist_pending) continue;
+            const hipError_t q = hipEventQuery(o.hist_ev);
+            if (q == hipSuccess) {
+                o.hist_pending = false;
+                R.hist.assign(o.h_hist, o.h_hist + o.hist_words);
+                R.hist_sig = o.hist_sig;
+            } else {
+                (void)hipGetLastError();  // hipErrorNotReady: not an error here
+                if (q != hipErrorNotReady) HIP_OK(q);
+            }
+        }
+#ifdef RS_NO_GRID_HINT  // (dev A/B: every carried launch over a block per 256 paths of the window)
+        const bool hint = false;
+#else
+        const bool hint = R.hist_sig == sig && R.hist.size() == hwords;
+#endif
+        if (L.hist_cap < hwords) {
+            if (L.h_hist) { HIP_OK(hipEventSynchronize(L.hist_ev)); HIP_OK(hipHostFree(L.h_hist)); L.h_hist = nullptr; }
+            HIP_OK(hipHostMalloc((void**)&L.h_hist, hwords * sizeof(uint32_t)));
+            L.hist_cap = hwords;
+            L.hist_pending = false;
+        }
+        if (!L.hist_ev) HIP_OK(hipEventCreateWithFlags(&L.hist_ev, hipEventDisableTiming));
         // every lane and the accumulate stream start after L0's dependencies and the counter reset
         hipStream_t ls[kMaxLanes] = {L0};
         for (uint32_t l = 1; l < f.lanes; ++l) ls[l] = lane_stream(L, l);
@@ -1896,6 +1945,10 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      return;
                  }
                  auto extend = [&](int part, uint64_t n_max) {
+                     if (hint && part == kExtCarried) {
+                         const uint64_t est = R.hist[hoff[l] + t];
+                         n_max = std::min<uint64_t>(n_max, est + est / 4 + 64ull * kBlock);
+                     }
                      const uint32_t b = (uint32_t)std::min<uint64_t>(ext_cap, (n_max + kBlock - 1) / kBlock);
                      if (!b) return;
                      HIP_OK(launch_wfs_extend(ds, dc, pp, WS, qd, (uint32_t)t, I, L.d_rad, b, part, sm, cs,
@@ -1918,7 +1971,14 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      extend(kExtAll, window[l] + n_new);
                  }
                  if (D > 0) {
-                     const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (window[l] + n_new + kBlock - 1) / kBlock);
+                     uint64_t n_sh = window[l] + n_new;  // the paths it may shade: at most the live ones
+#ifndef RS_NO_SHADE_HINT  // (dev A/B)
+                     if (hint) {
+                         const uint64_t est = R.hist[hoff[l] + t];
+                         n_sh = std::min<uint64_t>(n_sh, est + est / 4 + 64ull * kBlock + n_new);
+                     }
+#endif
+                     const uint32_t b = (uint32_t)std::min<uint64_t>(wide, (n_sh + kBlock - 1) / kBlock);
                      HIP_OK(launch_wfs_shade_all(ds, WS, qd, s->class_mask, (uint32_t)t, D, L.d_rad, b,
                                                  split_shade, sm, cs));
                      ++path_launches;
@@ -1953,6 +2013,16 @@ void render_enqueue(const rs_scene* s, Replica& R, const rs_camera_desc* cam, co
                      }
                      HIP_OK(hipEventRecord(L.fork_ev, L0));
                      HIP_OK(hipStreamWaitEvent(S, L.fork_ev, 0));
+                     // the frame's carried counts (counter slot 0 of each lane's iterations) for later frames' grids,
+                     // before the accumulate zeroes them
+                     for (uint32_t l = 0; l < f.lanes; ++l)
+                         HIP_OK(hipMemcpy2DAsync(L.h_hist + hoff[l], sizeof(uint32_t), L.d_counts + f.lane[l].cnt_off,
+                                                 kWfsStride * sizeof(uint32_t), sizeof(uint32_t), f.lane[l].T,
+                                                 hipMemcpyDeviceToHost, S));
+                     HIP_OK(hipEventRecord(L.hist_ev, S));
+                     L.hist_pending = true;
+                     L.hist_sig = sig;
+                     L.hist_words = hwords;
                      const size_t nz = counted ? 0 : n_counts;
                      HIP_OK(launch_accumulate(rk, L.d_acc, n_pix, planes, kl == 0, 1, fp, out, L.d_counts,
                                               (uint32_t)nz, S));

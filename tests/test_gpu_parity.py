@@ -622,3 +622,29 @@ def test_render_device_passes_stream(gpu, name):
                 assert np.array_equal(last.cpu().numpy(), singles[0])
         ds.set_workspace(32 << 20, 256 << 20)
         ds.set_lanes(0)
+
+
+def test_carried_grid_hint_from_a_lighter_frame(gpu):
+    """The carried-extend and shading grids of a streaming frame are sized from the carried counts of the last
+    completed frame of the same shape (rs_host.cpp Replica::hist); where the frame carries more paths than that
+    estimate the blocks grid-stride over the rest. A frame looking at the sky (almost nothing carried) then one of
+    the same shape looking at the balls (most paths carried): the second equals the oracle's frame bit for bit, and
+    so does a third with a history of its own shape."""
+    torch = gpu
+    from raysnail_amd.api import CameraBuilder, Point3
+    cam, world, _, _ = scenes.rtow_13_1(96, 60)
+    sky = CameraBuilder().look_from(Point3(13.0, 2.0, 3.0)).look_at(Point3(13.0, 50.0, 3.0)).vup((1.0, 0.0, 0.0)) \
+        .fov(20.0).width(96).height(60).build()
+    ds = world.device_scene()
+    ds.set_workspace(96 * 60, 96 * 60 * 16)  # several batches and iterations per frame
+    s = torch.cuda.current_stream().cuda_stream
+    st = cam.take_photo().samples(16).depth(12).seed(3).settings()
+    ref, rs = _oracle(world).render(cam.desc, st, threads=16)
+    out = torch.zeros((60, 96, 4), dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        ds.render_device(sky.desc, st, out.data_ptr(), s, stats=False)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        stats = ds.render_device(cam.desc, st, out.data_ptr(), s)
+        assert stats.segments == rs.segments
+        assert np.array_equal(out.cpu().numpy(), ref)
