@@ -175,8 +175,11 @@ constexpr int kCntFront = 6, kCntBack = 7;
 // 1 the carried paths, 2 the camera samples (ext_split: two launches per iteration). ev0 / ev1 (may be
 // null): start / stop events carried by the dispatch itself (hipExtLaunchKernel: no separate packets).
 constexpr int kExtAll = 0, kExtCarried = 1, kExtCamera = 2;
-// nest-2 scenes extend in two launches: the merged kernel needs 256 VGPRs + 2 AGPRs (one wave/SIMD)
-constexpr bool ext_split(int sm) { return sm == kSmNest2; }
+// nest-2 scenes extend in two launches: the merged kernel needs 256 VGPRs + 2 AGPRs (one wave/SIMD); the spheres
+// mode too since its carried launches take grids from the last frame's counts (rs_host.cpp Replica::hist) and its
+// carried part runs at 5 waves: a C3-shaped frame (1920x1080x64, depth 50) 42.4 -> 41.1 ms
+// (profiles/r6/ab/ext_split_spheres_r6h5.jsonl; nest-0 example.sdl equal, so it keeps the merged launch)
+constexpr bool ext_split(int sm) { return sm == kSmNest2 || sm == kSmSpheres; }
 hipError_t launch_wfs_extend(const SceneRef& s, const DCamera& c, const PathParams& p, const WfState& w,
                              QEnt* const* queues, uint32_t it, const InjParams& inj, double* rad, uint32_t blocks,
                              int part, int sm, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

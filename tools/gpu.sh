@@ -238,6 +238,16 @@ for s in "$@"; do
       (cd $R && echo "== $n" >> $OUT/libtrace.txt && python3 tools/trace_sum.py $(ls $OUT/lt_$n/*kernel_trace.csv) 2 >> $OUT/libtrace.txt)
     done
     cat $OUT/libtrace.txt ;;
+  splitab)
+    # the streaming extend in two launches on iterations with carried paths and camera samples (dev RS_EXT_SPLIT=1)
+    # against the product: C2-, C3-shaped frames and the C5-like small rtow frame, 2 rounds
+    for rep in 1 2; do
+      for sc in "example 64 50 800x500" "rtow 64 50 1920x1080" "rtow 16 50 800x500"; do
+        (cd $R && step 300 python3 tools/time_scene.py $R/raysnail_amd/lib/libraysnail_hip.so $sc >> $OUT/splitab.jsonl 2>> $OUT/splitab.err) || { echo "split ab failed"; tail -5 $OUT/splitab.err; exit 1; }
+        (cd $R && RS_HIP_LIB=$R/raysnail_amd/lib/libraysnail_hip_dev.so RS_EXT_SPLIT=1 step 300 python3 tools/time_scene.py $R/raysnail_amd/lib/libraysnail_hip_dev.so $sc >> $OUT/splitab.jsonl 2>> $OUT/splitab.err) || { echo "split ab dev failed"; exit 1; }
+      done
+    done
+    cat $OUT/splitab.jsonl ;;
   configs)
     (cd $R && step 900 python3 tools/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err) || { echo "config sweep failed"; tail -5 $OUT/configs.err; exit 1; }
     cat $OUT/configs.jsonl ;;
