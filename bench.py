@@ -244,14 +244,34 @@ def main():
         # one rank's work at N = K: the row lattice 0::K of the same frame (render_sharded's split)
         K = args.row_share
         ns = max(args.steps, 30)  # share frames are ~1 ms: more of them for a steadier clock
-        for _ in range(args.warmup):
-            render(0, 0, K, 0)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(ns):
-            render(0, 0, K, 0)
-        torch.cuda.synchronize()
-        sh_ms = (time.perf_counter() - t1) / ns * 1e3
+        # the share frames alone and with rank 0's gather work after each (distributed.gather_rows: pack copy,
+        # the world's packed rows arriving -- a same-size device copy stands in for RCCL's writes --,
+        # de-interleave), pipelined like the real job's: the gather of frame f overlaps frame f+1's path kernels.
+        # The two loops alternate, 3 runs each, and each reports its median run: timed one after the other, the
+        # second loop also paid for whatever state the first left (round 6 read 40-54 us of "gather" that way,
+        # against 7 us for the three copies in a pipelined probe, profiles/r6/ab/gather_probe_r6d.txt)
+        gather = GatherProxy(frame, K)
+
+        def share_loop(with_gather):
+            for _ in range(args.warmup):
+                render(0, 0, K, 0)
+                if with_gather:
+                    gather()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(ns):
+                render(0, 0, K, 0)
+                if with_gather:
+                    gather()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t1) / ns * 1e3
+
+        runs = {False: [], True: []}
+        for _ in range(3):
+            for g in (False, True):
+                runs[g].append(share_loop(g))
+        sh_ms = sorted(runs[False])[1]
+        shg_ms = sorted(runs[True])[1]
         ds.set_lanes(1)
         timed["on"] = True
         sh_launch_ms = 0.0
@@ -260,20 +280,6 @@ def main():
             sh_launch_ms += last["stats"].kernel_ms
         timed["on"] = False
         ds.set_lanes(LANES)
-        # the same share frames with rank 0's gather work after each (distributed.gather_rows: pack copy, the
-        # world's packed rows arriving -- a same-size device copy stands in for RCCL's writes --, de-interleave),
-        # pipelined like the real job's: the gather of frame f overlaps frame f+1's path kernels
-        gather = GatherProxy(frame, K)
-        for _ in range(args.warmup):
-            render(0, 0, K, 0)
-            gather()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(ns):
-            render(0, 0, K, 0)
-            gather()
-        torch.cuda.synchronize()
-        shg_ms = (time.perf_counter() - t1) / ns * 1e3
         # the xGMI leg the proxy's device copy cannot show: each peer's packed rows over its own link into rank
         # 0 (links in parallel), at the per-link figure the task states (7 links x ~153 GB/s per GPU)
         per_rank_bytes = len(range(0, H, K)) * W * 16
@@ -287,6 +293,8 @@ def main():
                                  f"{per_rank_bytes} B per peer over one xGMI link at 153 GB/s ({xgmi_ms:.4f} ms)",
                  "predicted_efficiency": round(eff_g, 4),
                  "predicted_speedup": round(K * eff_g, 3),
+                 "runs_ms": [round(x, 4) for x in runs[False]],
+                 "runs_with_gather_ms": [round(x, 4) for x in runs[True]],
                  "extend_ms_per_share": round(sh_launch_ms / ns, 4), "share_frames_timed": ns,
                  "samples_per_share": int(last["stats"].samples), "launches_per_share": int(last["stats"].launches)}
 
