@@ -1291,29 +1291,57 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
 }
 
 // Camera-ray order: the i-th camera sample a launch traces is item gen_perm(i) of its batch (whole
-// sample planes). Within each plane the lattice pixels are visited in TW x TH tiles (TW * TH = 64:
-// one wave traces one compact pixel tile, whose camera rays take nearly the same BVH path; a 64 x 1
-// row strip spans 8x the angle across -- bench frame 10.21 -> 9.89 ms), the pixels outside the whole
-// tiles after them in row-major order. Pure scheduling: rad[] is indexed by item, so the frame does
-// not depend on it. A batch that is not whole planes keeps the identity order.
+// sample planes). A wave traces SP samples of each of 64 / SP lattice pixels: the batch's planes are cut into
+// groups of RS_PIX_SAMPLES planes and the rest into groups of decreasing powers of two (15 planes: 8, 4, 2, 1),
+// and inside a group of SP planes the i-th sample is plane i % SP of pixel i / SP in the pixels' tile order. The
+// camera rays of one pixel differ by the sub-pixel jitter and the lens disk only, so a wave of one pixel's
+// samples walks nearly one ray's nodes, and its hits, scattered rays and shading records stay together in the
+// later iterations' queues. Against one sample plane per wave (round 6): 32 samples of 2 pixels per wave, bench frame
+// 6.344 -> 6.212 ms, N = 8 share 0.900 -> 0.843 ms; 64 / 16 / 8 samples 6.260 / 6.226 / 6.232 ms; a C3-shaped frame
+// 41.6 -> 40.8 ms; C4, C5, C2 and X1 shapes equal (profiles/r7/ab/pix_samples_r7c.txt, _scenes_r7c.jsonl). The pixels are visited in TW x TH tiles (TW * TH = 64 / SP; with one sample per
+// pixel a 64 x 1 row strip spans 8x the angle of an 8 x 8 tile -- bench frame 10.21 -> 9.89 ms in round 2), the
+// pixels outside the whole tiles after them in row-major order. Pure scheduling: rad[] is indexed by item, so
+// the frame does not depend on it. A batch that is not whole planes keeps the identity order.
+#ifndef RS_PIX_SAMPLES
+#define RS_PIX_SAMPLES 32u
+#endif
 __device__ __forceinline__ uint32_t gen_perm(uint32_t i, uint64_t item0, uint32_t n, const PathParams& P) {
+    const uint32_t npl = P.n_pix_local, W = P.width;
+    if ((item0 % npl) != 0 || (n % npl) != 0) return i;
+    constexpr uint32_t M = RS_PIX_SAMPLES;  // a power of two <= 64
+    const uint32_t planes = n / npl, nfull = planes / M;
+    uint32_t SP = M, p0, r;  // i's group: its planes, first plane, and i's index inside it
+    if (i < nfull * M * npl) {
+        const uint32_t g = i / (M * npl);
+        p0 = g * M;
+        r = i - g * (M * npl);
+    } else {
+        p0 = nfull * M;
+        r = i - p0 * npl;
+        uint32_t left = planes - p0;  // 1 .. M - 1
+        SP = 1u << (31u - __clz(left));
+        while (r >= SP * npl) {
+            r -= SP * npl;
+            p0 += SP;
+            left -= SP;
+            SP = 1u << (31u - __clz(left));
+        }
+    }
+    const uint32_t TP = 64u / SP;  // pixels per wave
     // A lattice with row step k (a strong-scaled share: rows r, r + k, ...) puts TH lattice rows
-    // TH * k screen rows apart: keep the tile near square on screen (step >= 8: 16 x 4, 4-7: 32 x 2, 2-3: 16 x 4)
-    uint32_t TW = 8, TH = 8;
+    // TH * k screen rows apart: keep the tile near square on screen (64-pixel tiles: step >= 8: 16 x 4,
+    // 4-7: 32 x 2, 2-3: 16 x 4; step 1: 8 x 8)
+    uint32_t TH = 1u << ((31u - __clz(TP)) / 2);
 #ifndef RS_SHARE_TH8
 #define RS_SHARE_TH8 4u  // lattice rows per tile at row step >= 8 (16 x 4 lattice = 16 x 25 screen px at step 8; 64 x 1: N = 8 share 0.9416 -> 0.9313 ms, 32 x 2: 0.9342; profiles/r6/ab/variants_r6c_leaf2_th.txt)
 #endif
-    if (P.row_step > 1) {
-        TH = P.row_step >= 8 ? RS_SHARE_TH8 : P.row_step >= 4 ? 2u : 4u;
-        TW = 64u / TH;
-    }
-    const uint32_t npl = P.n_pix_local, W = P.width;
-    if ((item0 % npl) != 0 || (n % npl) != 0) return i;
-    const uint32_t s = i / npl;
-    uint32_t q = i - s * npl, pl;
+    if (P.row_step > 1) TH = min(TH, P.row_step >= 8 ? RS_SHARE_TH8 : P.row_step >= 4 ? 2u : 4u);
+    const uint32_t TW = TP / TH;
+    const uint32_t s = p0 + r % SP;  // sample plane
+    uint32_t q = r / SP, pl;         // the pixel's position in the tile order
     const uint32_t R = npl / W, Wt = W - W % TW, Rt = R - R % TH, nt = Wt * Rt;
     if (q < nt) {
-        const uint32_t t = q / 64u, k = q % 64u, tpr = Wt / TW;
+        const uint32_t t = q / TP, k = q % TP, tpr = Wt / TW;
         const uint32_t ty = t / tpr, tx = t - ty * tpr;
         pl = (ty * TH + k / TW) * W + tx * TW + k % TW;
     } else {
