@@ -1296,12 +1296,12 @@ __device__ __forceinline__ bool camera_sample(const DCamera& C, const PathParams
 // and inside a group of SP planes the i-th sample is plane i % SP of pixel i / SP in the pixels' tile order. The
 // camera rays of one pixel differ by the sub-pixel jitter and the lens disk only, so a wave of one pixel's
 // samples walks nearly one ray's nodes, and its hits, scattered rays and shading records stay together in the
-// later iterations' queues. Against one sample plane per wave (round 6): 32 samples of 2 pixels per wave, bench frame
-// 6.344 -> 6.212 ms, N = 8 share 0.900 -> 0.843 ms; 64 / 16 / 8 samples 6.260 / 6.226 / 6.232 ms; a C3-shaped frame
-// 41.6 -> 40.8 ms; C4, C5, C2 and X1 shapes equal (profiles/r7/ab/pix_samples_r7c.txt, _scenes_r7c.jsonl). The pixels are visited in TW x TH tiles (TW * TH = 64 / SP; with one sample per
-// pixel a 64 x 1 row strip spans 8x the angle of an 8 x 8 tile -- bench frame 10.21 -> 9.89 ms in round 2), the
-// pixels outside the whole tiles after them in row-major order. Pure scheduling: rad[] is indexed by item, so
-// the frame does not depend on it. A batch that is not whole planes keeps the identity order.
+// later iterations' queues. Against one sample plane per wave (round 6): 32 samples of 2 pixels per wave, bench
+// frame 6.344 -> 6.212 ms, N = 8 share 0.900 -> 0.843 ms; 64 / 16 / 8 samples 6.260 / 6.226 / 6.232 ms; a C3-shaped
+// frame 41.6 -> 40.8 ms; C4, C5, C2 and X1 shapes equal (profiles/r6/ab/pix_samples_r7c.txt, _scenes_r7c.jsonl).
+// The pixels are visited in TW x TH tiles (TW * TH = 64 / SP; with one sample per pixel a 64 x 1 row strip spans
+// 8x the angle of an 8 x 8 tile -- bench frame 10.21 -> 9.89 ms in round 2), the pixels outside the whole tiles
+// after them in row-major order. Pure scheduling: rad[] is indexed by item, so the frame does not depend on it. A batch that is not whole planes keeps the identity order.
 #ifndef RS_PIX_SAMPLES
 #define RS_PIX_SAMPLES 32u
 #endif
@@ -1966,6 +1966,8 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
     }
     // light-sample rays (camera.rs:196-205, all aimed at the few lights) fill the next set from
     // the front, the rest from the back: the next extend's waves then trace rays of one kind
+    // (the other rays binned by direction sign inside each block's back-run slots, 2 / 4 / 8 bins: bench frame -0.6 /
+    // 0.0 / +0.4 %, the N = 8 share and C2 / C3 shapes unchanged: profiles/r6/ab/bsdf_bins_r7d.txt, not kept)
     uint32_t* const gc[2] = {&cnt_next[cix(kCntBack)], &cnt_next[cix(kCntFront)]};
     const uint32_t slot = block_slot<2>(alive ? light_ray : -1, gc);
     if (alive) {
