@@ -1686,9 +1686,7 @@ constexpr int kClsLight = 6;
 // 7.58 -> 7.31 ms. Its camera part keeps 4 (13 VGPRs would spill).
 constexpr int ext_min_waves(int sm, bool lobj = false, int part = kExtAll) {
     if (sm == kSmSpheres && part == kExtCarried) return 5;
-#ifdef RS_CAM_WAVES
-    if (sm == kSmSpheres && part == kExtCamera) return RS_CAM_WAVES;
-#endif
+    // (the spheres camera part at 5 waves spills 108 B: bench frame +4 %, profiles/r6/ab/waves_cam_lean_r7i.txt)
     return sm == kSmNest2 ? (lobj ? 3 : 2) : 4;
 }
 
@@ -1993,10 +1991,8 @@ __device__ __forceinline__ void wfs_shade_batch(const DScene& S, const WfState& 
 template <int SM, bool G4, bool LOBJ, int PS>
 // (the nest-2 lean launch at 3 waves, no scratch: C4-shaped frame +0.4 %; at 5 waves +5.7 %:
 // profiles/r5/ab/n2_lean_waves_r6d.jsonl)
-#ifndef RS_LEAN_WAVES
-#define RS_LEAN_WAVES 4
-#endif
-#define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? (SM == kSmSpheres ? RS_LEAN_WAVES : 4) : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3)
+// (the spheres lean launch at 5 waves spills 136 B: bench frame +10 %, profiles/r6/ab/waves_cam_lean_r7i.txt)
+#define RS_SHADE_WAVES(SM, G4, LOBJ, PS) (PS == 1 ? 4 : (SM == kSmNest2 && G4 && !LOBJ) ? 1 : 3)
 __global__ __launch_bounds__(kBlock, RS_SHADE_WAVES(SM, G4, LOBJ, PS)) void k_wfs_shade_all(const DScene* __restrict__ Sp, WfState W,
                                                                                    QEnt* const* __restrict__ queues,
                                                                                    uint32_t class_mask, uint32_t it,
