@@ -161,6 +161,27 @@ def test_determinism_batching_and_rows(gpu, monkeypatch, mode):
     assert np.array_equal(a, out)
 
 
+def test_camera_order_plane_groups(gpu):
+    """gen_perm (rs_kernels.hip): a wave traces 32 samples of each of 2 pixels, a batch's sample planes cut into
+    groups of 32 and then of decreasing powers of two (49 planes: 32 + 16 + 1). Pure scheduling: the frame equals
+    the one rendered one plane per batch (single-plane groups, the old one-plane-per-wave order), and a row share at
+    N = 8 (2 x 1 pixel tiles) renders its rows as the full frame does."""
+    cam, world, _, _ = scenes.rtow_13_1(72, 45)
+    photo = cam.take_photo().samples(49).depth(8).seed(5)
+    a = photo.shot(None, world)
+    cam2, world2, _, _ = scenes.rtow_13_1(72, 45)
+    world2.device_scene().set_workspace(max_batch_items=72 * 45)
+    b = cam2.take_photo().samples(49).depth(8).seed(5).shot(None, world2)
+    assert np.array_equal(a, b)
+    ds = world.device_scene()
+    out = np.zeros_like(a)
+    ds.render(cam.desc, photo.rows(1, 0, 8).settings(), out=out)
+    assert np.array_equal(a[1::8], out[1::8])
+    ref, _ = _oracle(world).render(cam.desc, photo.rows(0, 0, 9).settings())
+    rmse, exact, mx = _cmp(a[0::9], ref[0::9])
+    assert rmse < 1e-4 and exact >= 0.999, (rmse, exact, mx)
+
+
 def test_pixel_mask_and_untouched_rows(gpu):
     """painter.rs:204-210: pixels the PixelController rejects come back [0,0,0,0]."""
     cam, world = scenes.example_sdl(64, 40)
