@@ -231,6 +231,7 @@ struct Replica {
     DScene uploaded{};                      // the copy last written to d_ds
     std::vector<uint32_t> hist;             // the latest completed streaming frame's carried counts (Slot::h_hist)
     uint64_t hist_sig = 0;                  // and its schedule's signature
+    std::vector<hipStream_t> pad_streams;   // dev A/B only (RS_PAD_STREAMS)
 
     // wait until no frame of this replica is in flight (before a shared buffer is replaced)
     void quiesce() {
@@ -253,6 +254,7 @@ struct Replica {
         const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
         for (Slot& sl : slots) sl.release();  // an asynchronous frame may still read the scene
         if (stream) (void)hipStreamSynchronize(stream);
+        for (hipStream_t st : pad_streams) (void)hipStreamDestroy(st);
         for (void* p : dev) (void)hipFree(p);
         for (void* p : {(void*)d_ovf, (void*)d_ds})
             if (p) (void)hipFree(p);
@@ -809,6 +811,14 @@ void upload_replica(rs_scene* s, int device) {
     HIP_OK(hipMalloc((void**)&R->d_ds, sizeof(DScene)));
     std::memset(&R->uploaded, 0xff, sizeof(DScene));  // forces the first upload
     HIP_OK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
+#ifdef RS_DEV_KNOBS  // dev A/B: idle streams created before the slots' streams (they shift HIP's stream -> hardware queue map)
+    if (const char* e = std::getenv("RS_PAD_STREAMS"))
+        for (int k = std::atoi(e); k > 0; --k) {
+            hipStream_t st;
+            HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            R->pad_streams.push_back(st);
+        }
+#endif
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
     R->n_cu = prop.multiProcessorCount;
